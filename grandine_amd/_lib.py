@@ -1,0 +1,156 @@
+"""ctypes binding of the C ABI in include/grandine_bls_gpu.h.
+
+The shared library is built in-tree (grandine_amd/lib/libgrandine_bls.so) by
+``__graft_entry__.build()`` / ``make -C grandine_amd``.  There is no CPU fallback:
+if the library or a gfx950 device is missing, calls raise ``EngineUnavailable``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgrandine_bls.so")
+
+# status codes (BLST_ERROR mirror)
+SUCCESS = 0
+BAD_ENCODING = 1
+POINT_NOT_ON_CURVE = 2
+POINT_NOT_IN_GROUP = 3
+AGGR_TYPE_MISMATCH = 4
+VERIFY_FAIL = 5
+PK_IS_INFINITY = 6
+BAD_SCALAR = 7
+ERR_NO_DEVICE = 100
+
+P1_BYTES = 96
+P2_BYTES = 192
+FP12_BYTES = 576
+
+EXPORTS = [
+    "gbls_init",
+    "gbls_last_error",
+    "gbls_version",
+    "gbls_g1_decompress",
+    "gbls_g2_decompress",
+    "gbls_g2_validate",
+    "gbls_g1_compress",
+    "gbls_g2_compress",
+    "gbls_g1_aggregate",
+    "gbls_g1_aggregate_segments",
+    "gbls_g2_aggregate",
+    "gbls_verify",
+    "gbls_fast_aggregate_verify",
+    "gbls_aggregate_verify_batch",
+    "gbls_fast_aggregate_verify_batch",
+    "gbls_multi_verify",
+    "gbls_multi_verify_segments",
+    "gbls_multi_verify_segments_device",
+    "gbls_multi_verify_partials_device",
+    "gbls_final_verify_partials_device",
+    "gbls_sk_to_pk",
+    "gbls_sign",
+    "gbls_hash_to_g2",
+    "gbls_measure_mad64_peak",
+]
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+_ready = False
+
+_c = ctypes
+_u8p = _c.c_char_p
+_sz = _c.c_size_t
+_vp = _c.c_void_p
+
+
+def load_library():
+    """Load the shared library without touching the GPU (symbol checks only)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise EngineUnavailable(f"{LIB_PATH} not built (run __graft_entry__.build())")
+            lib = _c.CDLL(LIB_PATH)
+            sig = {
+                "gbls_init": (_c.c_int, [_c.c_uint32, _c.c_uint32]),
+                "gbls_last_error": (_c.c_int, []),
+                "gbls_version": (_c.c_char_p, []),
+                "gbls_g1_decompress": (_c.c_int, [_vp, _sz, _c.c_int, _vp, _vp]),
+                "gbls_g2_decompress": (_c.c_int, [_vp, _sz, _vp, _vp]),
+                "gbls_g2_validate": (_c.c_int, [_vp, _sz, _vp]),
+                "gbls_g1_compress": (_c.c_int, [_vp, _sz, _vp]),
+                "gbls_g2_compress": (_c.c_int, [_vp, _sz, _vp]),
+                "gbls_g1_aggregate": (_c.c_int, [_vp, _sz, _vp]),
+                "gbls_g1_aggregate_segments": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
+                "gbls_g2_aggregate": (_c.c_int, [_vp, _sz, _vp]),
+                "gbls_verify": (_c.c_int, [_vp, _vp, _sz, _vp]),
+                "gbls_fast_aggregate_verify": (_c.c_int, [_vp, _vp, _sz, _vp, _sz]),
+                "gbls_aggregate_verify_batch": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
+                "gbls_fast_aggregate_verify_batch": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+                "gbls_multi_verify": (_c.c_int, [_vp, _vp, _vp, _vp, _sz]),
+                "gbls_multi_verify_segments": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp]),
+                "gbls_multi_verify_segments_device": (
+                    _c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp]),
+                "gbls_multi_verify_partials_device": (
+                    _c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp]),
+                "gbls_final_verify_partials_device": (_c.c_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
+                "gbls_sk_to_pk": (_c.c_int, [_vp, _sz, _vp]),
+                "gbls_sign": (_c.c_int, [_vp, _vp, _vp, _sz, _vp]),
+                "gbls_hash_to_g2": (_c.c_int, [_vp, _vp, _sz, _vp, _sz, _vp]),
+                "gbls_measure_mad64_peak": (_c.c_double, []),
+            }
+            for name, (res, args) in sig.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def lib():
+    """The library with the device initialised (raises if no gfx950 device)."""
+    global _ready
+    L = load_library()
+    if not _ready:
+        with _lock:
+            if not _ready:
+                if L.gbls_init(0, 0) != SUCCESS:
+                    raise EngineUnavailable(
+                        f"gbls_init failed (error {L.gbls_last_error()}): no usable gfx950 device")
+                _ready = True
+    return L
+
+
+def buf(data: bytes):
+    """A ctypes buffer holding ``data`` (kept alive by the caller)."""
+    return _c.create_string_buffer(bytes(data), len(data) or 1)
+
+
+def addr(b) -> int:
+    return _c.addressof(b)
+
+
+def check(rc: int, what: str):
+    if rc != SUCCESS:
+        raise EngineUnavailable(f"{what} failed: rc={rc} err={lib().gbls_last_error()}")
+
+
+def i32_array(n: int):
+    return (_c.c_int32 * max(n, 1))()
+
+
+def u32_array(vals):
+    vals = list(vals)
+    return (_c.c_uint32 * max(len(vals), 1))(*vals)
+
+
+def u64_array(vals):
+    vals = list(vals)
+    return (_c.c_uint64 * max(len(vals), 1))(*vals)

@@ -1,0 +1,450 @@
+// G1 (E: y^2 = x^3 + 4 over Fp) and G2 (E': y^2 = x^3 + 4(1+u) over Fp2) arithmetic.
+//
+// Replaces blst's POINTonE1 / POINTonE2 layer used by PublicKey::aggregate
+// (bls/src/public_key.rs:34-55), decompression (public_key.rs:16-31,
+// signature.rs:36-45), compression (public_key.rs:9-14, signature.rs:29-34) and the
+// 64-bit random-scalar multiplications inside verify_multiple_aggregate_signatures
+// (signature.rs:117-126).  Jacobian coordinates (x = X/Z^2, y = Y/Z^3), Z = 0 is the
+// point at infinity; affine infinity is all-zero limbs, as in blst.
+#pragma once
+#include "bls_field.h"
+
+namespace gbls {
+
+// ----- overload set so one template serves Fp and Fp2 curves
+HD void f_add(fp &r, const fp &a, const fp &b) { fp_add(r, a, b); }
+HD void f_sub(fp &r, const fp &a, const fp &b) { fp_sub(r, a, b); }
+HD void f_mul(fp &r, const fp &a, const fp &b) { fp_mul(r, a, b); }
+HD void f_sqr(fp &r, const fp &a) { fp_sqr(r, a); }
+HD void f_neg(fp &r, const fp &a) { fp_neg(r, a); }
+HD void f_dbl(fp &r, const fp &a) { fp_add(r, a, a); }
+HD bool f_is_zero(const fp &a) { return fp_is_zero(a); }
+HD bool f_eq(const fp &a, const fp &b) { return fp_eq(a, b); }
+HD void f_one(fp &r) { fp_one(r); }
+HD void f_zero(fp &r) { fp_zero(r); }
+HD void f_inv(fp &r, const fp &a) { fp_inv(r, a); }
+HD void f_add(fp2 &r, const fp2 &a, const fp2 &b) { fp2_add(r, a, b); }
+HD void f_sub(fp2 &r, const fp2 &a, const fp2 &b) { fp2_sub(r, a, b); }
+HD void f_mul(fp2 &r, const fp2 &a, const fp2 &b) { fp2_mul(r, a, b); }
+HD void f_sqr(fp2 &r, const fp2 &a) { fp2_sqr(r, a); }
+HD void f_neg(fp2 &r, const fp2 &a) { fp2_neg(r, a); }
+HD void f_dbl(fp2 &r, const fp2 &a) { fp2_add(r, a, a); }
+HD bool f_is_zero(const fp2 &a) { return fp2_is_zero(a); }
+HD bool f_eq(const fp2 &a, const fp2 &b) { return fp2_eq(a, b); }
+HD void f_one(fp2 &r) { fp2_one(r); }
+HD void f_zero(fp2 &r) { fp2_zero(r); }
+HD void f_inv(fp2 &r, const fp2 &a) { fp2_inv(r, a); }
+
+template <class F>
+struct jac {
+  F x, y, z;
+};
+template <class F>
+struct aff {
+  F x, y;
+};
+typedef jac<fp> g1j;
+typedef jac<fp2> g2j;
+typedef aff<fp> g1a;
+typedef aff<fp2> g2a;
+
+template <class F>
+HD bool aff_is_inf(const aff<F> &a) {
+  return f_is_zero(a.x) && f_is_zero(a.y);
+}
+template <class F>
+HD bool jac_is_inf(const jac<F> &a) {
+  return f_is_zero(a.z);
+}
+template <class F>
+HD void jac_set_inf(jac<F> &r) {
+  f_one(r.x);
+  f_one(r.y);
+  f_zero(r.z);
+}
+template <class F>
+HD void jac_from_aff(jac<F> &r, const aff<F> &a) {
+  r.x = a.x;
+  r.y = a.y;
+  if (aff_is_inf(a))
+    f_zero(r.z);
+  else
+    f_one(r.z);
+}
+template <class F>
+HD void jac_neg(jac<F> &r, const jac<F> &a) {
+  r.x = a.x;
+  f_neg(r.y, a.y);
+  r.z = a.z;
+}
+
+// dbl-2009-l (a = 0): 2M + 5S
+template <class F>
+HD void jac_dbl(jac<F> &r, const jac<F> &p) {
+  F A, B, C, D, E, Fq, t;
+  f_sqr(A, p.x);
+  f_sqr(B, p.y);
+  f_sqr(C, B);
+  f_add(t, p.x, B);
+  f_sqr(t, t);
+  f_sub(t, t, A);
+  f_sub(t, t, C);
+  f_dbl(D, t);
+  f_dbl(E, A);
+  f_add(E, E, A);
+  f_sqr(Fq, E);
+  F z3;
+  f_mul(z3, p.y, p.z);
+  f_dbl(r.z, z3);
+  f_sub(r.x, Fq, D);
+  f_sub(r.x, r.x, D);
+  f_sub(t, D, r.x);
+  f_mul(t, E, t);
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_sub(r.y, t, C);
+}
+
+// add-2007-bl with the doubling / inverse / infinity cases handled
+template <class F>
+HD void jac_add(jac<F> &r, const jac<F> &p, const jac<F> &q) {
+  if (jac_is_inf(p)) {
+    r = q;
+    return;
+  }
+  if (jac_is_inf(q)) {
+    r = p;
+    return;
+  }
+  F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t;
+  f_sqr(z1z1, p.z);
+  f_sqr(z2z2, q.z);
+  f_mul(u1, p.x, z2z2);
+  f_mul(u2, q.x, z1z1);
+  f_mul(s1, p.y, q.z);
+  f_mul(s1, s1, z2z2);
+  f_mul(s2, q.y, p.z);
+  f_mul(s2, s2, z1z1);
+  f_sub(h, u2, u1);
+  f_sub(rr, s2, s1);
+  if (f_is_zero(h)) {
+    if (f_is_zero(rr)) {
+      jac_dbl(r, p);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  f_dbl(i, h);
+  f_sqr(i, i);
+  f_mul(j, h, i);
+  f_dbl(rr, rr);
+  f_mul(v, u1, i);
+  jac<F> o;
+  f_sqr(o.x, rr);
+  f_sub(o.x, o.x, j);
+  f_sub(o.x, o.x, v);
+  f_sub(o.x, o.x, v);
+  f_sub(t, v, o.x);
+  f_mul(t, rr, t);
+  f_mul(s1, s1, j);
+  f_dbl(s1, s1);
+  f_sub(o.y, t, s1);
+  f_add(t, p.z, q.z);
+  f_sqr(t, t);
+  f_sub(t, t, z1z1);
+  f_sub(t, t, z2z2);
+  f_mul(o.z, t, h);
+  r = o;
+}
+
+// madd-2007-bl: p Jacobian + q affine (q not infinity)
+template <class F>
+HD void jac_add_aff(jac<F> &r, const jac<F> &p, const aff<F> &q) {
+  if (aff_is_inf(q)) {
+    r = p;
+    return;
+  }
+  if (jac_is_inf(p)) {
+    jac_from_aff(r, q);
+    return;
+  }
+  F z1z1, u2, s2, h, hh, i, j, rr, v, t;
+  f_sqr(z1z1, p.z);
+  f_mul(u2, q.x, z1z1);
+  f_mul(s2, q.y, p.z);
+  f_mul(s2, s2, z1z1);
+  f_sub(h, u2, p.x);
+  f_sub(rr, s2, p.y);
+  if (f_is_zero(h)) {
+    if (f_is_zero(rr)) {
+      jac_dbl(r, p);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  f_sqr(hh, h);
+  f_dbl(i, hh);
+  f_dbl(i, i);
+  f_mul(j, h, i);
+  f_dbl(rr, rr);
+  f_mul(v, p.x, i);
+  jac<F> o;
+  f_sqr(o.x, rr);
+  f_sub(o.x, o.x, j);
+  f_sub(o.x, o.x, v);
+  f_sub(o.x, o.x, v);
+  f_sub(t, v, o.x);
+  f_mul(t, rr, t);
+  f_mul(s2, p.y, j);
+  f_dbl(s2, s2);
+  f_sub(o.y, t, s2);
+  f_add(t, p.z, h);
+  f_sqr(t, t);
+  f_sub(t, t, z1z1);
+  f_sub(o.z, t, hh);
+  r = o;
+}
+
+template <class F>
+HD void jac_to_aff(aff<F> &r, const jac<F> &p) {
+  if (jac_is_inf(p)) {
+    f_zero(r.x);
+    f_zero(r.y);
+    return;
+  }
+  F zi, zi2, zi3;
+  f_inv(zi, p.z);
+  f_sqr(zi2, zi);
+  f_mul(zi3, zi2, zi);
+  f_mul(r.x, p.x, zi2);
+  f_mul(r.y, p.y, zi3);
+}
+
+// Jacobian equality without inversion: X1 Z2^2 == X2 Z1^2 and Y1 Z2^3 == Y2 Z1^3
+template <class F>
+HD bool jac_eq(const jac<F> &p, const jac<F> &q) {
+  bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  F z1z1, z2z2, a, b;
+  f_sqr(z1z1, p.z);
+  f_sqr(z2z2, q.z);
+  f_mul(a, p.x, z2z2);
+  f_mul(b, q.x, z1z1);
+  if (!f_eq(a, b)) return false;
+  f_mul(a, p.y, q.z);
+  f_mul(a, a, z2z2);
+  f_mul(b, q.y, p.z);
+  f_mul(b, b, z1z1);
+  return f_eq(a, b);
+}
+
+// [k]P for an affine base and a 64-bit scalar, MSB-first double-and-add.
+template <class F>
+HD void mul_u64(jac<F> &r, const aff<F> &base, uint64_t k) {
+  jac<F> acc;
+  jac_set_inf(acc);
+  if (k == 0 || aff_is_inf(base)) {
+    r = acc;
+    return;
+  }
+  int top = 63;
+  while (!((k >> top) & 1)) top--;
+  jac_from_aff(acc, base);
+  for (int i = top - 1; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    if ((k >> i) & 1) jac_add_aff(acc, acc, base);
+  }
+  r = acc;
+}
+
+// out-of-line general additions (segment sums, cofactor clearing, membership tests)
+HDNI void g1_add_n(g1j &r, const g1j &p, const g1j &q) { jac_add(r, p, q); }
+HDNI void g2_add_n(g2j &r, const g2j &p, const g2j &q) { jac_add(r, p, q); }
+HD void jac_add_n(g1j &r, const g1j &p, const g1j &q) { g1_add_n(r, p, q); }
+HD void jac_add_n(g2j &r, const g2j &p, const g2j &q) { g2_add_n(r, p, q); }
+
+// [|x|]P for a Jacobian point (|x| = 0xd201000000010000, 6 set bits) -- callers negate.
+template <class F>
+HD void mul_by_xabs(jac<F> &r, const jac<F> &p) {
+  jac<F> acc = p;
+  for (int i = 62; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    if ((k::X_ABS >> i) & 1) jac_add_n(acc, acc, p);
+  }
+  r = acc;
+}
+
+// ----- on-curve checks
+HD bool g1_on_curve(const g1a &a) {
+  fp l, rr;
+  fp_sqr(l, a.y);
+  fp_sqr(rr, a.x);
+  fp_mul(rr, rr, a.x);
+  fp_add(rr, rr, fp_const(k::B1_M));
+  return fp_eq(l, rr);
+}
+HD bool g2_on_curve(const g2a &a) {
+  fp2 l, rr;
+  fp2_sqr(l, a.y);
+  fp2_sqr(rr, a.x);
+  fp2_mul(rr, rr, a.x);
+  fp2_add(rr, rr, fp2_const(k::B2_C0, k::B2_C1));
+  return fp2_eq(l, rr);
+}
+
+// ----- endomorphisms
+// psi(x,y) = (conj(x) cx, conj(y) cy); on Jacobian coordinates Z is conjugated too.
+HD void g2_psi(g2j &r, const g2j &p) {
+  fp2 t;
+  fp2_conj(t, p.x);
+  fp2_mul(r.x, t, fp2_const(k::PSI_CX_C0, k::PSI_CX_C1));
+  fp2_conj(t, p.y);
+  fp2_mul(r.y, t, fp2_const(k::PSI_CY_C0, k::PSI_CY_C1));
+  fp2_conj(r.z, p.z);
+}
+HD void g2_psi2(g2j &r, const g2j &p) {
+  fp2_mul(r.x, p.x, fp2_const(k::PSI2_CX_C0, k::PSI2_CX_C1));
+  fp2_mul(r.y, p.y, fp2_const(k::PSI2_CY_C0, k::PSI2_CY_C1));
+  r.z = p.z;
+}
+
+// G2 membership (affine input, assumed on curve): psi(P) == [x]P  (x < 0)
+HD bool g2_in_group(const g2a &a) {
+  if (aff_is_inf(a)) return true;
+  g2j p, xp, pp;
+  jac_from_aff(p, a);
+  mul_by_xabs(xp, p);
+  jac_neg(xp, xp);
+  g2_psi(pp, p);
+  return jac_eq(pp, xp);
+}
+// G1 membership: phi(P) = (beta x, y) == [-x^2]P
+HD bool g1_in_group(const g1a &a) {
+  if (aff_is_inf(a)) return true;
+  g1j p, t;
+  jac_from_aff(p, a);
+  mul_by_xabs(t, p);
+  mul_by_xabs(t, t);
+  jac_neg(t, t);
+  g1j phi;
+  fp_mul(phi.x, a.x, fp_const(k::BETA_M));
+  phi.y = a.y;
+  fp_one(phi.z);
+  return jac_eq(phi, t);
+}
+
+// ----- serialization (ZCash / blst big-endian compressed form)
+HD void fp_from_be48(fp &r, const uint8_t *b) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint8_t *q = b + 4 * (11 - i);
+    r.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+HD void fp_to_be48(uint8_t *b, const fp &a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint8_t *q = b + 4 * (11 - i);
+    uint32_t v = a.l[i];
+    q[0] = v >> 24;
+    q[1] = v >> 16;
+    q[2] = v >> 8;
+    q[3] = v;
+  }
+}
+
+enum : int32_t {
+  ST_SUCCESS = 0,
+  ST_BAD_ENCODING = 1,
+  ST_NOT_ON_CURVE = 2,
+  ST_NOT_IN_GROUP = 3,
+  ST_AGGR_TYPE_MISMATCH = 4,
+  ST_VERIFY_FAIL = 5,
+  ST_PK_IS_INFINITY = 6,
+  ST_BAD_SCALAR = 7,
+};
+
+// blst POINTonE1_Uncompress_Z semantics
+HD int32_t g1_decompress(g1a &r, const uint8_t *in) {
+  f_zero(r.x);
+  f_zero(r.y);
+  uint8_t b0 = in[0];
+  if (!(b0 & 0x80)) return ST_BAD_ENCODING;
+  if (b0 & 0x40) {
+    uint32_t acc = b0 & 0x3f;
+    for (int i = 1; i < 48; i++) acc |= in[i];
+    return acc ? ST_BAD_ENCODING : ST_SUCCESS;
+  }
+  fp x;
+  fp_from_be48(x, in);
+  x.l[11] &= 0x1fffffffu;
+  if (!limbs_lt(x.l, k::P)) return ST_BAD_ENCODING;
+  fp_to_mont(x, x);
+  fp rhs, y;
+  fp_sqr(rhs, x);
+  fp_mul(rhs, rhs, x);
+  fp_add(rhs, rhs, fp_const(k::B1_M));
+  if (!fp_sqrt(y, rhs)) return ST_NOT_ON_CURVE;
+  if (fp_lex_largest(y) != (bool)(b0 & 0x20)) fp_neg(y, y);
+  r.x = x;
+  r.y = y;
+  if (fp_is_zero(x)) return ST_NOT_IN_GROUP;  // (0, +-2) has order 3
+  return ST_SUCCESS;
+}
+// blst POINTonE2_Uncompress_Z semantics (on-curve check only)
+HD int32_t g2_decompress(g2a &r, const uint8_t *in) {
+  f_zero(r.x);
+  f_zero(r.y);
+  uint8_t b0 = in[0];
+  if (!(b0 & 0x80)) return ST_BAD_ENCODING;
+  if (b0 & 0x40) {
+    uint32_t acc = b0 & 0x3f;
+    for (int i = 1; i < 96; i++) acc |= in[i];
+    return acc ? ST_BAD_ENCODING : ST_SUCCESS;
+  }
+  fp2 x;
+  fp_from_be48(x.c1, in);
+  x.c1.l[11] &= 0x1fffffffu;
+  fp_from_be48(x.c0, in + 48);
+  if (!limbs_lt(x.c1.l, k::P) || !limbs_lt(x.c0.l, k::P)) return ST_BAD_ENCODING;
+  fp_to_mont(x.c0, x.c0);
+  fp_to_mont(x.c1, x.c1);
+  fp2 rhs, y;
+  fp2_sqr(rhs, x);
+  fp2_mul(rhs, rhs, x);
+  fp2_add(rhs, rhs, fp2_const(k::B2_C0, k::B2_C1));
+  if (!fp2_sqrt(y, rhs)) return ST_NOT_ON_CURVE;
+  if (fp2_lex_largest(y) != (bool)(b0 & 0x20)) fp2_neg(y, y);
+  r.x = x;
+  r.y = y;
+  return ST_SUCCESS;
+}
+HD void g1_compress(uint8_t *out, const g1a &a) {
+  if (aff_is_inf(a)) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 48; i++) out[i] = 0;
+    return;
+  }
+  fp x;
+  fp_from_mont(x, a.x);
+  fp_to_be48(out, x);
+  out[0] |= 0x80 | (fp_lex_largest(a.y) ? 0x20 : 0);
+}
+HD void g2_compress(uint8_t *out, const g2a &a) {
+  if (aff_is_inf(a)) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 96; i++) out[i] = 0;
+    return;
+  }
+  fp x0, x1;
+  fp_from_mont(x1, a.x.c1);
+  fp_from_mont(x0, a.x.c0);
+  fp_to_be48(out, x1);
+  fp_to_be48(out + 48, x0);
+  out[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
+}
+
+}  // namespace gbls

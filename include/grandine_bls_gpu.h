@@ -1,0 +1,149 @@
+/* grandine_bls_gpu.h -- C ABI of the MI355X BLS12-381 signature engine.
+ *
+ * Drop-in boundary for Grandine's signature hot path.  The reference has no FFI of
+ * its own: its `bls` crate calls the blst 0.3.11 Rust bindings.  Each entry point
+ * below replaces one of those call sites (reference = /root/reference):
+ *
+ *   gbls_g1_decompress          PublicKey: TryFrom<PublicKeyBytes>   bls/src/public_key.rs:16-31
+ *                               (blst_p1_uncompress + PublicKey::validate)
+ *   gbls_g2_decompress          Signature: TryFrom<SignatureBytes>   bls/src/signature.rs:36-45
+ *   gbls_g1_compress            From<PublicKey> for PublicKeyBytes    bls/src/public_key.rs:9-14
+ *   gbls_g2_compress            From<Signature> for SignatureBytes    bls/src/signature.rs:29-34
+ *   gbls_g1_aggregate           PublicKey::aggregate_nonempty        bls/src/public_key.rs:34-55
+ *   gbls_g1_aggregate_segments  Triple::verify_aggregate (batched)   helper_functions/src/verifier.rs:387-405
+ *   gbls_g2_aggregate           Signature::aggregate                  bls/src/signature.rs:62-75
+ *   gbls_verify                 Signature::verify                     bls/src/signature.rs:47-60
+ *   gbls_fast_aggregate_verify  Signature::fast_aggregate_verify      bls/src/signature.rs:77-93
+ *   gbls_aggregate_verify_batch many independent verify calls         (SingleVerifier::extend, verifier.rs:215-236)
+ *   gbls_multi_verify           Signature::multi_verify               bls/src/signature.rs:95-129
+ *                               (reached from MultiVerifier::finish, verifier.rs:301-323)
+ *   gbls_multi_verify_segments  several independent multi_verify batches in one submission
+ *   gbls_sk_to_pk / gbls_sign   SecretKey::to_public_key / sign       bls/src/secret_key.rs:74-86
+ *
+ * Conventions
+ *   - gbls_p1_affine / gbls_p2_affine are byte-compatible with blst_p1_affine /
+ *     blst_p2_affine: little-endian limbs in Montgomery form (R = 2^384); all-zero
+ *     encodes the point at infinity.
+ *   - Status codes mirror BLST_ERROR.  Verification entry points return
+ *     GBLS_SUCCESS (valid) or GBLS_VERIFY_FAIL; any device/driver failure also
+ *     returns GBLS_VERIFY_FAIL (fail closed) and sets gbls_last_error().
+ *   - Host-pointer entry points are synchronous, reentrant and thread-safe; buffers
+ *     are borrowed for the call only.  *_device variants take device pointers
+ *     (inputs already resident in HBM) and are used by bench.py and the
+ *     multi-GPU path.
+ *   - There is NO CPU fallback inside this library: without a usable gfx950 device
+ *     every call fails with GBLS_ERR_NO_DEVICE.
+ */
+#ifndef GRANDINE_BLS_GPU_H
+#define GRANDINE_BLS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  uint64_t x[6], y[6];
+} gbls_p1_affine;
+typedef struct {
+  uint64_t x[2][6], y[2][6];
+} gbls_p2_affine;
+typedef struct {
+  uint64_t c[12][6]; /* Fp12 as 12 Fp limbs-vectors (tower order c0.c0.c0 ... c1.c2.c1) */
+} gbls_fp12;
+
+enum {
+  GBLS_SUCCESS = 0,
+  GBLS_BAD_ENCODING = 1,
+  GBLS_POINT_NOT_ON_CURVE = 2,
+  GBLS_POINT_NOT_IN_GROUP = 3,
+  GBLS_AGGR_TYPE_MISMATCH = 4,
+  GBLS_VERIFY_FAIL = 5,
+  GBLS_PK_IS_INFINITY = 6,
+  GBLS_BAD_SCALAR = 7,
+};
+/* side-channel error codes (gbls_last_error) */
+enum {
+  GBLS_ERR_NONE = 0,
+  GBLS_ERR_NO_DEVICE = 100,
+  GBLS_ERR_HIP = 101,
+  GBLS_ERR_ARG = 102,
+};
+
+int gbls_init(uint32_t device_mask, uint32_t flags);
+int gbls_last_error(void);
+const char *gbls_version(void);
+
+/* a9 / a8 / a10 */
+int gbls_g1_decompress(const uint8_t (*in)[48], size_t n, int validate, gbls_p1_affine *out,
+                       int32_t *status);
+int gbls_g2_decompress(const uint8_t (*in)[96], size_t n, gbls_p2_affine *out, int32_t *status);
+int gbls_g2_validate(const gbls_p2_affine *in, size_t n, int32_t *status); /* sig subgroup check */
+int gbls_g1_compress(const gbls_p1_affine *in, size_t n, uint8_t (*out)[48]);
+int gbls_g2_compress(const gbls_p2_affine *in, size_t n, uint8_t (*out)[96]);
+
+/* a4 / a5 / a11: n == 0 -> GBLS_AGGR_TYPE_MISMATCH */
+int gbls_g1_aggregate(const gbls_p1_affine *pks, size_t n, gbls_p1_affine *out);
+int gbls_g1_aggregate_segments(const gbls_p1_affine *pks, const uint32_t *seg_offsets, size_t nseg,
+                               gbls_p1_affine *out, int32_t *status);
+int gbls_g2_aggregate(const gbls_p2_affine *sigs, size_t n, gbls_p2_affine *out);
+
+/* a6 / a7: returns GBLS_SUCCESS iff the signature verifies (blst semantics:
+ * sig_groupcheck = true, pk_validate = false, infinite pk rejected). */
+int gbls_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
+                const gbls_p1_affine *pk);
+int gbls_fast_aggregate_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
+                               const gbls_p1_affine *pks, size_t n);
+/* m independent (sig, msg, pk) checks; messages packed in msg_data with msg_off[m+1];
+ * verdicts[i] = GBLS_SUCCESS or GBLS_VERIFY_FAIL. */
+int gbls_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
+                                const uint32_t *msg_off, const gbls_p1_affine *pks, size_t m,
+                                int32_t *verdicts);
+/* C3 shape: m fast_aggregate_verify calls, pks of message i = pks[seg_off[i] .. seg_off[i+1]) */
+int gbls_fast_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
+                                     const uint32_t *msg_off, const gbls_p1_affine *pks,
+                                     const uint32_t *seg_off, size_t m, int32_t *verdicts);
+
+/* a1: random-linear-combination batch verification with caller-supplied nonzero
+ * 64-bit scalars (bls/src/signature.rs:106-115 draws them); n == 0 -> VERIFY_FAIL
+ * (MultiVerifier::finish short-circuits n == 0 before calling, verifier.rs:303-305). */
+int gbls_multi_verify(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
+                      const gbls_p1_affine *pks, const uint64_t *rands, size_t n);
+/* nseg independent multi_verify batches: sets [seg_off[s], seg_off[s+1]) form batch s */
+int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
+                               const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
+                               const uint32_t *seg_off, size_t nseg, int32_t *verdicts);
+
+/* Device-pointer variants (all pointers are device memory; verdicts/partials too).
+ * stream may be NULL (the library's own stream).  Asynchronous: the caller syncs. */
+int gbls_multi_verify_segments_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
+                                      const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
+                                      const uint32_t *seg_off, size_t nseg, int32_t *verdicts,
+                                      void *stream);
+/* Multi-GPU split: per-segment Miller partial  F_s = prod_i ML(r_i pk_i, H(m_i)) * ML(-g1, S_s)
+ * (no final exponentiation) + per-segment error flags; then the product of k partials
+ * per segment and one final exponentiation. */
+int gbls_multi_verify_partials_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
+                                      const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
+                                      const uint32_t *seg_off, size_t nseg, gbls_fp12 *partials,
+                                      int32_t *seg_err, void *stream);
+int gbls_final_verify_partials_device(const gbls_fp12 *partials, const int32_t *seg_err,
+                                      size_t nparts, size_t nseg, int32_t *verdicts, void *stream);
+
+/* a15 (fixture generation): sk = 32-byte big-endian scalars < r */
+int gbls_sk_to_pk(const uint8_t (*sks)[32], size_t n, gbls_p1_affine *out);
+int gbls_sign(const uint8_t (*sks)[32], const uint8_t *msg_data, const uint32_t *msg_off, size_t n,
+              gbls_p2_affine *out);
+/* hash_to_G2 with an explicit DST (RFC 9380 test vectors) -> affine points */
+int gbls_hash_to_g2(const uint8_t *msg_data, const uint32_t *msg_off, size_t n, const uint8_t *dst,
+                    size_t dst_len, gbls_p2_affine *out);
+
+/* roofline helper: measured v_mad_u64_u32 throughput of this device (mad64/s) */
+double gbls_measure_mad64_peak(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
