@@ -260,19 +260,13 @@ HD void mul_u64(jac<F> &r, const aff<F> &base, uint64_t k) {
   r = acc;
 }
 
-// out-of-line general additions (segment sums, cofactor clearing, membership tests)
-HDNI void g1_add_n(g1j &r, const g1j &p, const g1j &q) { jac_add(r, p, q); }
-HDNI void g2_add_n(g2j &r, const g2j &p, const g2j &q) { jac_add(r, p, q); }
-HD void jac_add_n(g1j &r, const g1j &p, const g1j &q) { g1_add_n(r, p, q); }
-HD void jac_add_n(g2j &r, const g2j &p, const g2j &q) { g2_add_n(r, p, q); }
-
 // [|x|]P for a Jacobian point (|x| = 0xd201000000010000, 6 set bits) -- callers negate.
 template <class F>
 HD void mul_by_xabs(jac<F> &r, const jac<F> &p) {
   jac<F> acc = p;
   for (int i = 62; i >= 0; i--) {
     jac_dbl(acc, acc);
-    if ((k::X_ABS >> i) & 1) jac_add_n(acc, acc, p);
+    if ((k::X_ABS >> i) & 1) jac_add(acc, acc, p);
   }
   r = acc;
 }

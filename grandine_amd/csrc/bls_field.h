@@ -558,13 +558,4 @@ HD void fp12_frob2(fp12 &r, const fp12 &a) {
   fp2_mul_fp(r.c1.c2, a.c1.c2, fp_const(k::FROB2_5_M));
 }
 
-// Out-of-line Fp12 operations for code outside the Miller-loop hot loop (final
-// exponentiation, segment products): keeps kernels compact; operands go through the
-// lane's private segment, which is negligible next to ~10^4 VALU ops per call.
-HDNI void fp12_mul_n(fp12 &r, const fp12 &a, const fp12 &b) { fp12_mul(r, a, b); }
-HDNI void fp12_sqr_n(fp12 &r, const fp12 &a) { fp12_sqr(r, a); }
-HDNI void fp12_inv_n(fp12 &r, const fp12 &a) { fp12_inv(r, a); }
-HDNI void fp12_frob_n(fp12 &r, const fp12 &a) { fp12_frob(r, a); }
-HDNI void fp12_frob2_n(fp12 &r, const fp12 &a) { fp12_frob2(r, a); }
-
 }  // namespace gbls

@@ -217,7 +217,7 @@ HD void fp_from_be64_words(fp &r, const uint32_t *w) {
 // ---------------------------------------------------------------- SSWU + isogeny
 // Simplified SWU on E2': y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2), inversion-free up to
 // one final Fp2 inversion, returning a Jacobian point on E2'.
-HDNI void map_to_curve_sswu(g2j &out, const fp2 &u) {
+HD void map_to_curve_sswu(g2j &out, const fp2 &u) {
   const fp2 A = fp2_const(k::SSWU_A_C0, k::SSWU_A_C1);
   const fp2 B = fp2_const(k::SSWU_B_C0, k::SSWU_B_C1);
   const fp2 Z = fp2_const(k::SSWU_Z_C0, k::SSWU_Z_C1);
@@ -290,7 +290,7 @@ HDNI void map_to_curve_sswu(g2j &out, const fp2 &u) {
 
 // 3-isogeny E2' -> E2 on an affine-in-Jacobian (z = 1) input; Jacobian output
 // with Z = xd * yd:  X = xn xd yd^2,  Y = y yn xd^3 yd^2.
-HDNI void iso_map_g2(g2j &out, const g2j &in) {
+HD void iso_map_g2(g2j &out, const g2j &in) {
   const fp2 &x = in.x;
   fp2 x2, x3, xn, xd, yn, yd, t;
   fp2_sqr(x2, x);
@@ -336,7 +336,7 @@ HDNI void iso_map_g2(g2j &out, const g2j &in) {
 }
 
 // h_eff P = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P)   (RFC 9380 Appendix G.3 ordering)
-HDNI void clear_cofactor_g2(g2j &r, const g2j &p) {
+HD void clear_cofactor_g2(g2j &r, const g2j &p) {
   g2j t1, t2, t3, negp;
   mul_by_xabs(t1, p);
   jac_neg(t1, t1);  // t1 = [x]P
@@ -345,33 +345,42 @@ HDNI void clear_cofactor_g2(g2j &r, const g2j &p) {
   g2_psi2(t3, t3);  // t3 = psi^2(2P)
   g2j nt2;
   jac_neg(nt2, t2);
-  jac_add_n(t3, t3, nt2);  // t3 - t2
-  jac_add_n(t2, t1, t2);   // t1 + t2
+  jac_add(t3, t3, nt2);  // t3 - t2
+  jac_add(t2, t1, t2);   // t1 + t2
   mul_by_xabs(t2, t2);
   jac_neg(t2, t2);  // [x](t1 + t2)
-  jac_add_n(t3, t3, t2);
+  jac_add(t3, t3, t2);
   g2j nt1;
   jac_neg(nt1, t1);
-  jac_add_n(t3, t3, nt1);
+  jac_add(t3, t3, nt1);
   jac_neg(negp, p);
-  jac_add_n(r, t3, negp);
+  jac_add(r, t3, negp);
 }
 
-// hash_to_curve(msg) with DST, result as a Jacobian point on E2 (in G2)
-HDNI void hash_to_g2(g2j &r, const uint8_t *msg, uint32_t mlen, dst_ref dst) {
+// hash_to_field (RFC 9380 §5.2, count = 2, m = 2, L = 64): msg -> u[0], u[1] in Fp2
+HD void hash_to_field_g2(fp2 (&u)[2], const uint8_t *msg, uint32_t mlen, dst_ref dst) {
   uint32_t uni[64];
   expand_message_xmd_256(uni, msg, mlen, dst);
-  fp2 u0, u1;
-  fp_from_be64_words(u0.c0, uni + 0);
-  fp_from_be64_words(u0.c1, uni + 16);
-  fp_from_be64_words(u1.c0, uni + 32);
-  fp_from_be64_words(u1.c1, uni + 48);
-  g2j q0, q1, m;
-  map_to_curve_sswu(m, u0);
-  iso_map_g2(q0, m);
-  map_to_curve_sswu(m, u1);
-  iso_map_g2(q1, m);
-  jac_add_n(q0, q0, q1);
+  fp_from_be64_words(u[0].c0, uni + 0);
+  fp_from_be64_words(u[0].c1, uni + 16);
+  fp_from_be64_words(u[1].c0, uni + 32);
+  fp_from_be64_words(u[1].c1, uni + 48);
+}
+// map_to_curve (SSWU + 3-isogeny) of one field element -> Jacobian point on E2
+HD void map_to_g2(g2j &q, const fp2 &u) {
+  g2j m;
+  map_to_curve_sswu(m, u);
+  iso_map_g2(q, m);
+}
+// hash_to_curve(msg) with DST, result as a Jacobian point on E2 (in G2).  The device
+// pipeline runs the same three stages as separate kernels (k_h2c_*).
+HD void hash_to_g2(g2j &r, const uint8_t *msg, uint32_t mlen, dst_ref dst) {
+  fp2 u[2];
+  hash_to_field_g2(u, msg, mlen, dst);
+  g2j q0, q1;
+  map_to_g2(q0, u[0]);
+  map_to_g2(q1, u[1]);
+  jac_add(q0, q0, q1);
   clear_cofactor_g2(r, q0);
 }
 

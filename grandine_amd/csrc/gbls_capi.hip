@@ -51,7 +51,7 @@ struct Engine {
   int device = -1;
   hipStream_t stream = nullptr;
   // workspaces
-  Buf in0, in1, in2, in3, in4, in5, H, P, R, S, f, F, part, bad, err, out0, out1;
+  Buf in0, in1, in2, in3, in4, in5, in6, U, Q, H, P, R, f, part, bad, err, err2, FE, out0, out1;
 } g;
 
 bool fail(int code) {
@@ -115,56 +115,62 @@ bool sync() {
   return true;
 }
 
-// ----- multi_verify pipeline on device pointers (sets n, segments nseg)
-bool mv_partials(const uint8_t *msgs, const g2a *sigs, const g1a *pks, const uint64_t *rands,
-                 size_t n, const uint32_t *seg_off, size_t nseg, fp12 *partials, int32_t *seg_err,
-                 hipStream_t st) {
-  if (!g.H.ensure(n * sizeof(g2a)) || !g.P.ensure(n * sizeof(g1a)) ||
-      !g.R.ensure(n * sizeof(g2j)) || !g.f.ensure(n * sizeof(fp12)) ||
-      !g.bad.ensure(n * sizeof(int32_t)) || !g.S.ensure(nseg * sizeof(g2j)) ||
-      !g.F.ensure(nseg * sizeof(fp12)))
+// ----- the verification pipeline on device pointers.
+// Sets [0, n) grouped in segments by seg_off; per segment a Miller partial (no final
+// exponentiation) and an error flag.  rands == nullptr means r_i = 1 (single checks);
+// pre[i] != 0 marks a set that failed a pre-check (signature subgroup, aggregation).
+bool pipeline_partials(const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
+                       const g1a *pks, const uint64_t *rands, const int32_t *pre, size_t n,
+                       const uint32_t *seg_off, size_t nseg, fp12 *partials, int32_t *seg_err,
+                       hipStream_t st) {
+  size_t np = n + nseg;
+  if (!g.U.ensure(2 * n * sizeof(fp2)) || !g.Q.ensure(2 * n * sizeof(g2j)) ||
+      !g.H.ensure(np * sizeof(g2h)) || !g.P.ensure(np * sizeof(g1p)) ||
+      !g.R.ensure(n * sizeof(g2j)) || !g.f.ensure(np * sizeof(fp12)) ||
+      !g.bad.ensure(n * sizeof(int32_t)))
     return fail(GBLS_ERR_HIP);
   unsigned b = nblk(n);
-  k_hash_to_g2<<<b, WG, 0, st>>>(msgs, nullptr, (uint32_t)n, nullptr, 0, g.H.as<g2a>());
-  k_mv_g1mul<<<b, WG, 0, st>>>(pks, rands, (uint32_t)n, g.P.as<g1a>(), g.bad.as<int32_t>());
+  k_h2c_field<<<b, WG, 0, st>>>(msgs, msg_off, (uint32_t)n, nullptr, 0, g.U.as<fp2>());
+  k_h2c_map<<<nblk(2 * n), WG, 0, st>>>(g.U.as<fp2>(), (uint32_t)(2 * n), g.Q.as<g2j>());
+  k_h2c_clear<<<b, WG, 0, st>>>(g.Q.as<g2j>(), (uint32_t)n, g.H.as<g2h>());
+  k_mv_g1mul<<<b, WG, 0, st>>>(pks, rands, pre, (uint32_t)n, g.P.as<g1p>(), g.bad.as<int32_t>());
   k_mv_g2mul<<<b, WG, 0, st>>>(sigs, rands, (uint32_t)n, g.R.as<g2j>());
-  k_seg_g2_sum<<<(unsigned)nseg, WG, 0, st>>>(g.R.as<g2j>(), seg_off, (uint32_t)nseg, g.S.as<g2j>());
-  k_miller<<<b, WG, 0, st>>>(g.P.as<g1a>(), g.H.as<g2a>(), (uint32_t)n, g.f.as<fp12>());
-  k_seg_fp12_prod<<<(unsigned)nseg, WG, 0, st>>>(g.f.as<fp12>(), g.bad.as<int32_t>(), seg_off,
-                                                 (uint32_t)nseg, g.F.as<fp12>(), seg_err);
-  k_seg_partial<<<nblk(nseg), WG, 0, st>>>(g.F.as<fp12>(), g.S.as<g2j>(), (uint32_t)nseg, partials);
+  k_seg_g2_sum<<<(unsigned)nseg, WGR, 0, st>>>(g.R.as<g2j>(), seg_off, (uint32_t)nseg, (uint32_t)n,
+                                               g.P.as<g1p>(), g.H.as<g2h>());
+  k_miller<<<nblk(np), WG, 0, st>>>(g.P.as<g1p>(), g.H.as<g2h>(), (uint32_t)np, g.f.as<fp12>());
+  k_seg_fp12_prod<<<(unsigned)nseg, WGR, 0, st>>>(g.f.as<fp12>(), g.bad.as<int32_t>(), seg_off,
+                                                  (uint32_t)nseg, (uint32_t)n, partials, seg_err);
   HIPCHK(hipGetLastError());
   return true;
 }
 
-bool mv_segments_device(const uint8_t *msgs, const g2a *sigs, const g1a *pks,
-                        const uint64_t *rands, size_t n, const uint32_t *seg_off, size_t nseg,
-                        int32_t *verdicts, hipStream_t st) {
+// product of nparts partials per segment, final exponentiation, verdict per segment
+bool pipeline_final(const fp12 *partials, const int32_t *err, size_t nparts, size_t nseg,
+                    int32_t *verdicts, hipStream_t st) {
+  if (!g.FE.ensure(4 * nseg * sizeof(fp12)) || !g.err2.ensure(nseg * sizeof(int32_t)))
+    return fail(GBLS_ERR_HIP);
+  fp12 *F = g.FE.as<fp12>(), *A = F + nseg, *B = A + nseg, *T = B + nseg;
+  unsigned b = nblk(nseg);
+  uint32_t ns = (uint32_t)nseg;
+  k_fe_easy<<<b, WG, 0, st>>>(partials, err, (uint32_t)nparts, ns, F, g.err2.as<int32_t>());
+  k_fe_xm1<<<b, WG, 0, st>>>(F, ns, A);
+  k_fe_xm1<<<b, WG, 0, st>>>(A, ns, B);
+  k_fe_xpp<<<b, WG, 0, st>>>(B, ns, A);  // A <- B^(x+p)  ("B" of the chain)
+  k_fe_x<<<b, WG, 0, st>>>(A, ns, T);
+  k_fe_s5<<<b, WG, 0, st>>>(T, A, ns, B);  // B <- C
+  k_fe_s6<<<b, WG, 0, st>>>(B, F, g.err2.as<int32_t>(), ns, verdicts);
+  HIPCHK(hipGetLastError());
+  return true;
+}
+
+bool pipeline_verdicts(const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
+                       const g1a *pks, const uint64_t *rands, const int32_t *pre, size_t n,
+                       const uint32_t *seg_off, size_t nseg, int32_t *verdicts, hipStream_t st) {
   if (!g.part.ensure(nseg * sizeof(fp12)) || !g.err.ensure(nseg * sizeof(int32_t)))
     return fail(GBLS_ERR_HIP);
-  if (!mv_partials(msgs, sigs, pks, rands, n, seg_off, nseg, g.part.as<fp12>(),
-                   g.err.as<int32_t>(), st))
-    return false;
-  k_final_verify<<<nblk(nseg), WG, 0, st>>>(g.part.as<fp12>(), g.err.as<int32_t>(), 1,
-                                            (uint32_t)nseg, verdicts);
-  HIPCHK(hipGetLastError());
-  return true;
-}
-
-// ----- m independent pairing checks (sigs/pks/msgs already on device in in0..in3)
-bool av_batch_device(const g2a *sigs, const uint8_t *msg, const uint32_t *off, const g1a *pks,
-                     const int32_t *pre, size_t m, int32_t *verdicts_dev) {
-  if (!g.H.ensure(m * sizeof(g2a)) || !g.f.ensure(m * sizeof(fp12)) ||
-      !g.bad.ensure(m * sizeof(int32_t)))
-    return fail(GBLS_ERR_HIP);
-  unsigned b = nblk(m);
-  k_hash_to_g2<<<b, WG, 0, g.stream>>>(msg, off, (uint32_t)m, nullptr, 0, g.H.as<g2a>());
-  k_av_miller<<<b, WG, 0, g.stream>>>(sigs, pks, g.H.as<g2a>(), pre, (uint32_t)m, g.f.as<fp12>(),
-                                      g.bad.as<int32_t>());
-  k_final_verify<<<b, WG, 0, g.stream>>>(g.f.as<fp12>(), g.bad.as<int32_t>(), 1, (uint32_t)m,
-                                         verdicts_dev);
-  HIPCHK(hipGetLastError());
-  return true;
+  return pipeline_partials(msgs, msg_off, sigs, pks, rands, pre, n, seg_off, nseg,
+                           g.part.as<fp12>(), g.err.as<int32_t>(), st) &&
+         pipeline_final(g.part.as<fp12>(), g.err.as<int32_t>(), 1, nseg, verdicts, st);
 }
 
 }  // namespace
@@ -218,7 +224,7 @@ int gbls_g2_validate(const gbls_p2_affine *in, size_t n, int32_t *status) {
   if (n == 0) return GBLS_SUCCESS;
   if (!upload(g.in0, reinterpret_cast<const g2a *>(in), n) || !g.out1.ensure(n * sizeof(int32_t)))
     return -1;
-  k_g2_validate<<<nblk(n), WG, 0, g.stream>>>(g.in0.as<g2a>(), (uint32_t)n, g.out1.as<int32_t>());
+  k_g2_check<<<nblk(n), WG, 0, g.stream>>>(g.in0.as<g2a>(), (uint32_t)n, g.out1.as<int32_t>(), 0);
   if (!download(status, g.out1, n) || !sync()) return -1;
   return GBLS_SUCCESS;
 }
@@ -250,7 +256,7 @@ int gbls_g1_aggregate_segments(const gbls_p1_affine *pks, const uint32_t *seg_of
       !upload(g.in1, seg_offsets, nseg + 1) || !g.out0.ensure(nseg * sizeof(g1a)) ||
       !g.out1.ensure(nseg * sizeof(int32_t)))
     return -1;
-  k_g1_aggregate_seg<<<(unsigned)nseg, WG, 0, g.stream>>>(
+  k_g1_aggregate_seg<<<(unsigned)nseg, WGR, 0, g.stream>>>(
       g.in0.as<g1a>(), g.in1.as<uint32_t>(), (uint32_t)nseg, g.out0.as<g1a>(), g.out1.as<int32_t>());
   if (!download(reinterpret_cast<g1a *>(out), g.out0, nseg) || !download(status, g.out1, nseg) ||
       !sync())
@@ -275,25 +281,33 @@ int gbls_g2_aggregate(const gbls_p2_affine *sigs, size_t n, gbls_p2_affine *out)
   if (!upload(g.in0, reinterpret_cast<const g2a *>(sigs), n) || !upload(g.in1, off, 2) ||
       !g.out0.ensure(sizeof(g2a)))
     return -1;
-  k_g2_aggregate_seg<<<1, WG, 0, g.stream>>>(g.in0.as<g2a>(), g.in1.as<uint32_t>(), 1,
-                                             g.out0.as<g2a>());
+  k_g2_aggregate_seg<<<1, WGR, 0, g.stream>>>(g.in0.as<g2a>(), g.in1.as<uint32_t>(), 1,
+                                              g.out0.as<g2a>());
   if (!download(reinterpret_cast<g2a *>(out), g.out0, 1) || !sync()) return -1;
   return GBLS_SUCCESS;
 }
 
+// m independent checks e(pk_i, H(m_i)) == e(g1, sig_i), each its own segment
+// (r_i = 1), with the signature subgroup check folded into the pre-flags.
 int gbls_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                 const uint32_t *msg_off, const gbls_p1_affine *pks, size_t m,
                                 int32_t *verdicts) {
   API_LOCK
   if (m == 0) return GBLS_SUCCESS;
   for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
+  std::vector<uint32_t> ident(m + 1);
+  for (size_t i = 0; i <= m; i++) ident[i] = (uint32_t)i;
   if (!upload(g.in0, reinterpret_cast<const g2a *>(sigs), m) ||
-      !upload(g.in1, msg_data, msg_off[m]) || !upload(g.in2, msg_off, m + 1) ||
-      !upload(g.in3, reinterpret_cast<const g1a *>(pks), m) ||
-      !g.out1.ensure(m * sizeof(int32_t)))
+      !upload(g.in1, msg_data, msg_off[m] ? msg_off[m] : 1) || !upload(g.in2, msg_off, m + 1) ||
+      !upload(g.in3, reinterpret_cast<const g1a *>(pks), m) || !upload(g.in4, ident.data(), m + 1) ||
+      !g.in5.ensure(m * sizeof(int32_t)) || !g.out1.ensure(m * sizeof(int32_t)))
     return -1;
-  if (!av_batch_device(g.in0.as<g2a>(), g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), g.in3.as<g1a>(),
-                       nullptr, m, g.out1.as<int32_t>()))
+  if (hipMemsetAsync(g.in5.p, 0, m * sizeof(int32_t), g.stream) != hipSuccess)
+    return (t_last_error = GBLS_ERR_HIP), -1;
+  k_g2_check<<<nblk(m), WG, 0, g.stream>>>(g.in0.as<g2a>(), (uint32_t)m, g.in5.as<int32_t>(), 1);
+  if (!pipeline_verdicts(g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), g.in0.as<g2a>(), g.in3.as<g1a>(),
+                         nullptr, g.in5.as<int32_t>(), m, g.in4.as<uint32_t>(), m,
+                         g.out1.as<int32_t>(), g.stream))
     return -1;
   if (!download(verdicts, g.out1, m) || !sync()) {
     for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
@@ -319,17 +333,23 @@ int gbls_fast_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *
   if (m == 0) return GBLS_SUCCESS;
   for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
   size_t npk = seg_off[m];
+  std::vector<uint32_t> ident(m + 1);
+  for (size_t i = 0; i <= m; i++) ident[i] = (uint32_t)i;
   if (!upload(g.in0, reinterpret_cast<const g2a *>(sigs), m) ||
-      !upload(g.in1, msg_data, msg_off[m]) || !upload(g.in2, msg_off, m + 1) ||
-      !upload(g.in4, reinterpret_cast<const g1a *>(pks), npk) || !upload(g.in5, seg_off, m + 1) ||
+      !upload(g.in1, msg_data, msg_off[m] ? msg_off[m] : 1) || !upload(g.in2, msg_off, m + 1) ||
+      !upload(g.in4, reinterpret_cast<const g1a *>(pks), npk ? npk : 1) ||
+      !upload(g.in5, seg_off, m + 1) || !upload(g.in6, ident.data(), m + 1) ||
       !g.in3.ensure(m * sizeof(g1a)) || !g.out0.ensure(m * sizeof(int32_t)) ||
       !g.out1.ensure(m * sizeof(int32_t)))
     return -1;
-  k_g1_aggregate_seg<<<(unsigned)m, WG, 0, g.stream>>>(g.in4.as<g1a>(), g.in5.as<uint32_t>(),
-                                                       (uint32_t)m, g.in3.as<g1a>(),
-                                                       g.out0.as<int32_t>());
-  if (!av_batch_device(g.in0.as<g2a>(), g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), g.in3.as<g1a>(),
-                       g.out0.as<int32_t>(), m, g.out1.as<int32_t>()))
+  // aggregate pks per message (status AGGR_TYPE_MISMATCH for empty -> pre-flag)
+  k_g1_aggregate_seg<<<(unsigned)m, WGR, 0, g.stream>>>(g.in4.as<g1a>(), g.in5.as<uint32_t>(),
+                                                        (uint32_t)m, g.in3.as<g1a>(),
+                                                        g.out0.as<int32_t>());
+  k_g2_check<<<nblk(m), WG, 0, g.stream>>>(g.in0.as<g2a>(), (uint32_t)m, g.out0.as<int32_t>(), 1);
+  if (!pipeline_verdicts(g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), g.in0.as<g2a>(), g.in3.as<g1a>(),
+                         nullptr, g.out0.as<int32_t>(), m, g.in6.as<uint32_t>(), m,
+                         g.out1.as<int32_t>(), g.stream))
     return -1;
   if (!download(verdicts, g.out1, m) || !sync()) {
     for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
@@ -362,9 +382,9 @@ int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *
       !upload(g.in2, reinterpret_cast<const g1a *>(pks), n) || !upload(g.in3, rands, n) ||
       !upload(g.in4, seg_off, nseg + 1) || !g.out1.ensure(nseg * sizeof(int32_t)))
     return -1;
-  if (!mv_segments_device(g.in0.as<uint8_t>(), g.in1.as<g2a>(), g.in2.as<g1a>(),
-                          g.in3.as<uint64_t>(), n, g.in4.as<uint32_t>(), nseg,
-                          g.out1.as<int32_t>(), g.stream))
+  if (!pipeline_verdicts(g.in0.as<uint8_t>(), nullptr, g.in1.as<g2a>(), g.in2.as<g1a>(),
+                         g.in3.as<uint64_t>(), nullptr, n, g.in4.as<uint32_t>(), nseg,
+                         g.out1.as<int32_t>(), g.stream))
     return -1;
   if (!download(verdicts, g.out1, nseg) || !sync()) {
     for (size_t s = 0; s < nseg; s++) verdicts[s] = GBLS_VERIFY_FAIL;
@@ -392,9 +412,9 @@ int gbls_multi_verify_segments_device(const uint8_t *msgs, const gbls_p2_affine 
   API_LOCK
   if (nseg == 0) return GBLS_SUCCESS;
   hipStream_t st = stream ? (hipStream_t)stream : g.stream;
-  return mv_segments_device(msgs, reinterpret_cast<const g2a *>(sigs),
-                            reinterpret_cast<const g1a *>(pks), rands, n, seg_off, nseg, verdicts,
-                            st)
+  return pipeline_verdicts(msgs, nullptr, reinterpret_cast<const g2a *>(sigs),
+                           reinterpret_cast<const g1a *>(pks), rands, nullptr, n, seg_off, nseg,
+                           verdicts, st)
              ? GBLS_SUCCESS
              : -1;
 }
@@ -406,8 +426,9 @@ int gbls_multi_verify_partials_device(const uint8_t *msgs, const gbls_p2_affine 
   API_LOCK
   if (nseg == 0) return GBLS_SUCCESS;
   hipStream_t st = stream ? (hipStream_t)stream : g.stream;
-  return mv_partials(msgs, reinterpret_cast<const g2a *>(sigs), reinterpret_cast<const g1a *>(pks),
-                     rands, n, seg_off, nseg, reinterpret_cast<fp12 *>(partials), seg_err, st)
+  return pipeline_partials(msgs, nullptr, reinterpret_cast<const g2a *>(sigs),
+                           reinterpret_cast<const g1a *>(pks), rands, nullptr, n, seg_off, nseg,
+                           reinterpret_cast<fp12 *>(partials), seg_err, st)
              ? GBLS_SUCCESS
              : -1;
 }
@@ -417,9 +438,10 @@ int gbls_final_verify_partials_device(const gbls_fp12 *partials, const int32_t *
   API_LOCK
   if (nseg == 0) return GBLS_SUCCESS;
   hipStream_t st = stream ? (hipStream_t)stream : g.stream;
-  k_final_verify<<<nblk(nseg), WG, 0, st>>>(reinterpret_cast<const fp12 *>(partials), seg_err,
-                                            (uint32_t)nparts, (uint32_t)nseg, verdicts);
-  return hipGetLastError() == hipSuccess ? GBLS_SUCCESS : ((t_last_error = GBLS_ERR_HIP), -1);
+  return pipeline_final(reinterpret_cast<const fp12 *>(partials), seg_err, nparts, nseg, verdicts,
+                        st)
+             ? GBLS_SUCCESS
+             : -1;
 }
 
 int gbls_sk_to_pk(const uint8_t (*sks)[32], size_t n, gbls_p1_affine *out) {
@@ -431,17 +453,28 @@ int gbls_sk_to_pk(const uint8_t (*sks)[32], size_t n, gbls_p1_affine *out) {
   return GBLS_SUCCESS;
 }
 
+// hash_to_G2 of n messages into g.out1 (affine), optional custom DST
+static bool h2c_affine_locked(const uint8_t *msg_data, const uint32_t *msg_off, size_t n,
+                              const uint8_t *dst_dev, uint32_t dst_len) {
+  if (!upload(g.in1, msg_data, msg_off[n] ? msg_off[n] : 1) || !upload(g.in2, msg_off, n + 1) ||
+      !g.U.ensure(2 * n * sizeof(fp2)) || !g.Q.ensure(2 * n * sizeof(g2j)) ||
+      !g.H.ensure(n * sizeof(g2h)) || !g.out1.ensure(n * sizeof(g2a)))
+    return false;
+  k_h2c_field<<<nblk(n), WG, 0, g.stream>>>(g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), (uint32_t)n,
+                                            dst_dev, dst_len, g.U.as<fp2>());
+  k_h2c_map<<<nblk(2 * n), WG, 0, g.stream>>>(g.U.as<fp2>(), (uint32_t)(2 * n), g.Q.as<g2j>());
+  k_h2c_clear<<<nblk(n), WG, 0, g.stream>>>(g.Q.as<g2j>(), (uint32_t)n, g.H.as<g2h>());
+  k_g2h_to_aff<<<nblk(n), WG, 0, g.stream>>>(g.H.as<g2h>(), (uint32_t)n, g.out1.as<g2a>());
+  return hipGetLastError() == hipSuccess || fail(GBLS_ERR_HIP);
+}
+
 int gbls_sign(const uint8_t (*sks)[32], const uint8_t *msg_data, const uint32_t *msg_off, size_t n,
               gbls_p2_affine *out) {
   API_LOCK
   if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, &sks[0][0], 32 * n) || !upload(g.in1, msg_data, msg_off[n] ? msg_off[n] : 1) ||
-      !upload(g.in2, msg_off, n + 1) || !g.H.ensure(n * sizeof(g2a)) ||
-      !g.out0.ensure(n * sizeof(g2a)))
-    return -1;
-  k_hash_to_g2<<<nblk(n), WG, 0, g.stream>>>(g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), (uint32_t)n,
-                                             nullptr, 0, g.H.as<g2a>());
-  k_sign<<<nblk(n), WG, 0, g.stream>>>(g.in0.as<uint8_t>(), g.H.as<g2a>(), (uint32_t)n,
+  if (!upload(g.in0, &sks[0][0], 32 * n) || !g.out0.ensure(n * sizeof(g2a))) return -1;
+  if (!h2c_affine_locked(msg_data, msg_off, n, nullptr, 0)) return -1;
+  k_sign<<<nblk(n), WG, 0, g.stream>>>(g.in0.as<uint8_t>(), g.out1.as<g2a>(), (uint32_t)n,
                                        g.out0.as<g2a>());
   if (!download(reinterpret_cast<g2a *>(out), g.out0, n) || !sync()) return -1;
   return GBLS_SUCCESS;
@@ -452,13 +485,9 @@ int gbls_hash_to_g2(const uint8_t *msg_data, const uint32_t *msg_off, size_t n, 
   API_LOCK
   if (n == 0) return GBLS_SUCCESS;
   if (dst_len > 255) return (t_last_error = GBLS_ERR_ARG), -1;
-  if (!upload(g.in1, msg_data, msg_off[n] ? msg_off[n] : 1) || !upload(g.in2, msg_off, n + 1) ||
-      !upload(g.in3, dst, dst_len ? dst_len : 1) || !g.out0.ensure(n * sizeof(g2a)))
-    return -1;
-  k_hash_to_g2<<<nblk(n), WG, 0, g.stream>>>(g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), (uint32_t)n,
-                                             g.in3.as<uint8_t>(), (uint32_t)dst_len,
-                                             g.out0.as<g2a>());
-  if (!download(reinterpret_cast<g2a *>(out), g.out0, n) || !sync()) return -1;
+  if (!upload(g.in3, dst, dst_len ? dst_len : 1)) return -1;
+  if (!h2c_affine_locked(msg_data, msg_off, n, g.in3.as<uint8_t>(), (uint32_t)dst_len)) return -1;
+  if (!download(reinterpret_cast<g2a *>(out), g.out1, n) || !sync()) return -1;
   return GBLS_SUCCESS;
 }
 

@@ -1,18 +1,23 @@
 // Device kernels of the MI355X BLS12-381 engine (gfx950).
 //
-// Layout in HBM: every per-set intermediate is an array-of-structures of 32-bit
-// limbs (g1a 96 B, g2a 192 B, g2j 288 B, fp12 576 B).  One lane owns one set; a
-// wave processes 64 consecutive sets, so each lane's 16-byte vector loads of its own
-// element hit consecutive cache lines across the wave.  The work is VALU-integer
-// bound (~10^6 mad64 per set against ~200 B of input), so the layout is chosen for
-// simplicity of the per-lane code rather than for HBM bandwidth.
+// Execution model: one lane owns one signature set (or one hash-to-field element,
+// or one segment for the reductions).  All field arithmetic is inlined into small
+// stage kernels -- each stage keeps its working set (<= ~3 Fp12 values plus
+// temporaries) in the unified 512-entry VGPR/AGPR file at one wave per SIMD, and
+// hands its result to the next stage through HBM.
+//
+// Layout in HBM: per-set intermediates are arrays of structures of 32-bit limbs
+// (g1p 144 B, g2h 288 B, g2j 288 B, fp12 576 B).  A set needs ~10^6 mad64 against
+// ~2 KB of intermediate traffic, so the stages are VALU bound and the layout is
+// chosen for simple per-lane code, not for bandwidth (roofline).
 #pragma once
 #include "bls_hash.h"
 #include "bls_pairing.h"
 
 namespace gbls {
 
-constexpr int WG = 64;  // one wave per workgroup: the per-lane state is ~300 VGPRs
+constexpr int WG = 64;    // per-lane kernels: one wave per workgroup
+constexpr int WGR = 256;  // segment reductions: 4 waves, LDS tree
 
 __device__ __constant__ uint8_t DST_POP[43] = {
     'B', 'L', 'S', '_', 'S', 'I', 'G', '_', 'B', 'L', 'S', '1', '2', '3', '8', '1',
@@ -30,6 +35,11 @@ __device__ __forceinline__ void msg_ref(const uint8_t *data, const uint32_t *off
     p = data + 32u * i;
     len = 32;
   }
+}
+
+__device__ __forceinline__ void neg_g1_gen(g1a &a) {
+  fp_set(a.x, k::G1X_M);
+  fp_set(a.y, k::G1NEGY_M);
 }
 
 // ---------------------------------------------------------------- decode / encode
@@ -67,11 +77,18 @@ __global__ void __launch_bounds__(WG) k_g2_decompress(const uint8_t *in, uint32_
   st[i] = s;
 }
 
-__global__ void __launch_bounds__(WG) k_g2_validate(const g2a *in, uint32_t n, int32_t *st) {
+// signature subgroup check (sig_groupcheck = true in verify / fast_aggregate_verify);
+// infinity passes.  st[i] |= 1 on failure when `accumulate`, else st[i] = status.
+__global__ void __launch_bounds__(WG) k_g2_check(const g2a *in, uint32_t n, int32_t *st,
+                                                 int accumulate) {
   uint32_t i = gtid();
   if (i >= n) return;
   g2a a = in[i];
-  st[i] = (g2_on_curve(a) || aff_is_inf(a)) && g2_in_group(a) ? ST_SUCCESS : ST_NOT_IN_GROUP;
+  bool ok = aff_is_inf(a) || (g2_on_curve(a) && g2_in_group(a));
+  if (accumulate)
+    st[i] = st[i] | (ok ? 0 : 1);
+  else
+    st[i] = ok ? ST_SUCCESS : ST_NOT_IN_GROUP;
 }
 
 __global__ void __launch_bounds__(WG) k_g1_compress(const g1a *in, uint32_t n, uint8_t *out) {
@@ -86,31 +103,30 @@ __global__ void __launch_bounds__(WG) k_g2_compress(const g2a *in, uint32_t n, u
 }
 
 // ---------------------------------------------------------------- segmented sums
-// Workgroup reduction of one Jacobian point per lane through LDS (result in lane 0).
+// Workgroup tree reduction of one Jacobian point per lane through LDS (result: lane 0)
 template <class F>
 __device__ void wg_reduce_jac(jac<F> &v) {
-  __shared__ jac<F> buf[WG];
-  buf[threadIdx.x] = v;
-  __syncthreads();
-  for (int s = WG / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < (unsigned)s) {
-      jac<F> o = buf[threadIdx.x + s];
-      jac_add_n(v, v, o);
-      buf[threadIdx.x] = v;
-    }
+  __shared__ jac<F> buf[WGR / 2];
+  for (int w = WGR / 2; w > 0; w >>= 1) {
     __syncthreads();
+    if (threadIdx.x >= (unsigned)w && threadIdx.x < (unsigned)2 * w) buf[threadIdx.x - w] = v;
+    __syncthreads();
+    if (threadIdx.x < (unsigned)w) {
+      jac<F> o = buf[threadIdx.x];
+      jac_add(v, v, o);
+    }
   }
 }
 
 // one workgroup per segment: pks[off[s] .. off[s+1]) -> affine sum (a4/a5)
-__global__ void __launch_bounds__(WG) k_g1_aggregate_seg(const g1a *pks, const uint32_t *off,
-                                                         uint32_t nseg, g1a *out, int32_t *st) {
+__global__ void __launch_bounds__(WGR) k_g1_aggregate_seg(const g1a *pks, const uint32_t *off,
+                                                          uint32_t nseg, g1a *out, int32_t *st) {
   uint32_t s = blockIdx.x;
   if (s >= nseg) return;
   uint32_t b = off[s], e = off[s + 1];
   g1j acc;
   jac_set_inf(acc);
-  for (uint32_t i = b + threadIdx.x; i < e; i += WG) jac_add_aff(acc, acc, pks[i]);
+  for (uint32_t i = b + threadIdx.x; i < e; i += WGR) jac_add_aff(acc, acc, pks[i]);
   wg_reduce_jac(acc);
   if (threadIdx.x == 0) {
     g1a r;
@@ -120,14 +136,14 @@ __global__ void __launch_bounds__(WG) k_g1_aggregate_seg(const g1a *pks, const u
   }
 }
 
-__global__ void __launch_bounds__(WG) k_g2_aggregate_seg(const g2a *pts, const uint32_t *off,
-                                                         uint32_t nseg, g2a *out) {
+__global__ void __launch_bounds__(WGR) k_g2_aggregate_seg(const g2a *pts, const uint32_t *off,
+                                                          uint32_t nseg, g2a *out) {
   uint32_t s = blockIdx.x;
   if (s >= nseg) return;
   uint32_t b = off[s], e = off[s + 1];
   g2j acc;
   jac_set_inf(acc);
-  for (uint32_t i = b + threadIdx.x; i < e; i += WG) jac_add_aff(acc, acc, pts[i]);
+  for (uint32_t i = b + threadIdx.x; i < e; i += WGR) jac_add_aff(acc, acc, pts[i]);
   wg_reduce_jac(acc);
   if (threadIdx.x == 0) {
     g2a r;
@@ -136,35 +152,74 @@ __global__ void __launch_bounds__(WG) k_g2_aggregate_seg(const g2a *pts, const u
   }
 }
 
-// ---------------------------------------------------------------- multi_verify stages
-// H_i = hash_to_G2(m_i), affine
-__global__ void __launch_bounds__(WG) k_hash_to_g2(const uint8_t *msg, const uint32_t *off,
-                                                   uint32_t n, const uint8_t *dst, uint32_t dlen,
-                                                   g2a *H) {
+// ---------------------------------------------------------------- hash_to_G2 stages
+// stage 1: expand_message_xmd + hash_to_field -> u[0], u[1]
+__global__ void __launch_bounds__(WG) k_h2c_field(const uint8_t *msg, const uint32_t *off,
+                                                  uint32_t n, const uint8_t *dst, uint32_t dlen,
+                                                  fp2 *U) {
   uint32_t i = gtid();
   if (i >= n) return;
   const uint8_t *p;
   uint32_t len;
   msg_ref(msg, off, i, p, len);
-  g2j h;
-  hash_to_g2(h, p, len, dst_ref{dst ? dst : DST_POP, dst ? dlen : 43u});
+  fp2 u[2];
+  hash_to_field_g2(u, p, len, dst_ref{dst ? dst : DST_POP, dst ? dlen : 43u});
+  U[2 * i] = u[0];
+  U[2 * i + 1] = u[1];
+}
+// stage 2: one lane per field element: SSWU on E2' + 3-isogeny -> Jacobian on E2
+__global__ void __launch_bounds__(WG) k_h2c_map(const fp2 *U, uint32_t nu, g2j *Q) {
+  uint32_t i = gtid();
+  if (i >= nu) return;
+  g2j q;
+  map_to_g2(q, U[i]);
+  Q[i] = q;
+}
+// stage 3: Q0 + Q1, clear cofactor -> homogeneous projective H (Miller-loop input)
+__global__ void __launch_bounds__(WG) k_h2c_clear(const g2j *Q, uint32_t n, g2h *H) {
+  uint32_t i = gtid();
+  if (i >= n) return;
+  g2j a = Q[2 * i], b = Q[2 * i + 1], h;
+  jac_add(a, a, b);
+  clear_cofactor_g2(h, a);
+  g2h o;
+  g2h_from_jac(o, h);
+  H[i] = o;
+}
+// homogeneous -> affine (API outputs, signing)
+__global__ void __launch_bounds__(WG) k_g2h_to_aff(const g2h *H, uint32_t n, g2a *out) {
+  uint32_t i = gtid();
+  if (i >= n) return;
+  g2h h = H[i];
   g2a a;
-  jac_to_aff(a, h);
-  H[i] = a;
+  if (fp2_is_zero(h.z)) {
+    fp2_zero(a.x);
+    fp2_zero(a.y);
+  } else {
+    fp2 zi;
+    fp2_inv(zi, h.z);
+    fp2_mul(a.x, h.x, zi);
+    fp2_mul(a.y, h.y, zi);
+  }
+  out[i] = a;
 }
 
-// P_i = affine(r_i pk_i); bad_i = pk_i is infinity (blst PAIRING_Aggregate_PK_in_G1)
-__global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t *rands, uint32_t n,
-                                                 g1a *P, int32_t *bad) {
+// ---------------------------------------------------------------- batch-verify stages
+// P_i = r_i pk_i in Miller form; bad_i = pk infinite (blst PAIRING_Aggregate_PK_in_G1)
+// or a caller pre-check failed (signature subgroup check, aggregation status).
+__global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t *rands,
+                                                 const int32_t *pre, uint32_t n, g1p *P,
+                                                 int32_t *bad) {
   uint32_t i = gtid();
   if (i >= n) return;
   g1a pk = pks[i];
+  uint64_t r = rands ? rands[i] : 1;
   g1j t;
-  mul_u64(t, pk, rands[i]);
-  g1a a;
-  jac_to_aff(a, t);
-  P[i] = a;
-  bad[i] = aff_is_inf(pk) ? 1 : 0;
+  mul_u64(t, pk, r);
+  g1p o;
+  g1p_from_jac(o, t);
+  P[i] = o;
+  bad[i] = (aff_is_inf(pk) || (pre && pre[i] != 0)) ? 1 : 0;
 }
 
 // R_i = r_i sig_i (Jacobian); infinite signatures contribute the identity
@@ -173,132 +228,139 @@ __global__ void __launch_bounds__(WG) k_mv_g2mul(const g2a *sigs, const uint64_t
   uint32_t i = gtid();
   if (i >= n) return;
   g2j t;
-  mul_u64(t, sigs[i], rands[i]);
+  mul_u64(t, sigs[i], rands ? rands[i] : 1);
   R[i] = t;
 }
 
-// S_s = sum of R_i over segment s (one workgroup per segment)
-__global__ void __launch_bounds__(WG) k_seg_g2_sum(const g2j *R, const uint32_t *off,
-                                                   uint32_t nseg, g2j *S) {
+// S_s = sum R_i over segment s; writes the segment's extra Miller pair (-g1, S_s)
+// at index n + s of the pair arrays.
+__global__ void __launch_bounds__(WGR) k_seg_g2_sum(const g2j *R, const uint32_t *off,
+                                                    uint32_t nseg, uint32_t n, g1p *P, g2h *H) {
   uint32_t s = blockIdx.x;
   if (s >= nseg) return;
   g2j acc;
   jac_set_inf(acc);
-  for (uint32_t i = off[s] + threadIdx.x; i < off[s + 1]; i += WG) jac_add_n(acc, acc, R[i]);
+  for (uint32_t i = off[s] + threadIdx.x; i < off[s + 1]; i += WGR) {
+    g2j r = R[i];
+    jac_add(acc, acc, r);
+  }
   wg_reduce_jac(acc);
-  if (threadIdx.x == 0) S[s] = acc;
+  if (threadIdx.x == 0) {
+    g1a ng1;
+    neg_g1_gen(ng1);
+    g1p pp;
+    g1p_from_aff(pp, ng1);
+    g2h q;
+    g2h_from_jac(q, acc);
+    P[n + s] = pp;
+    H[n + s] = q;
+  }
 }
 
-// f_i = MillerLoop(P_i, H_i)
-__global__ void __launch_bounds__(WG) k_miller(const g1a *P, const g2a *H, uint32_t n, fp12 *f) {
+// f_i = MillerLoop(P_i, H_i) over all pairs (sets and per-segment extra pairs)
+__global__ void __launch_bounds__(WG) k_miller(const g1p *P, const g2h *H, uint32_t npairs,
+                                               fp12 *f) {
   uint32_t i = gtid();
-  if (i >= n) return;
+  if (i >= npairs) return;
   fp12 r;
   miller_loop(r, P[i], H[i]);
   f[i] = r;
 }
 
-// F_s = prod f_i over segment s; err_s = OR of bad_i (one workgroup per segment)
-__global__ void __launch_bounds__(WG) k_seg_fp12_prod(const fp12 *f, const int32_t *bad,
-                                                      const uint32_t *off, uint32_t nseg,
-                                                      fp12 *F, int32_t *err) {
+// partial_s = f[n+s] * prod f_i over segment s;  err_s = OR bad_i | empty segment
+__global__ void __launch_bounds__(WGR) k_seg_fp12_prod(const fp12 *f, const int32_t *bad,
+                                                       const uint32_t *off, uint32_t nseg,
+                                                       uint32_t n, fp12 *part, int32_t *err) {
+  __shared__ fp12 buf[WGR / 2];
   __shared__ int32_t e_sh;
   uint32_t s = blockIdx.x;
   if (s >= nseg) return;
   if (threadIdx.x == 0) e_sh = 0;
   __syncthreads();
   fp12 acc;
-  fp12_one(acc);
+  if (threadIdx.x == 0)
+    acc = f[n + s];
+  else
+    fp12_one(acc);
   int32_t e = 0;
-  for (uint32_t i = off[s] + threadIdx.x; i < off[s + 1]; i += WG) {
-    fp12_mul_n(acc, acc, f[i]);
+  for (uint32_t i = off[s] + threadIdx.x; i < off[s + 1]; i += WGR) {
+    fp12 x = f[i];
+    fp12_mul(acc, acc, x);
     e |= bad[i];
   }
   if (e) atomicOr(&e_sh, 1);
-  // tree product through LDS, 16 lanes at a time to bound LDS use (576 B per element)
-  __shared__ fp12 buf[16];
-  for (int base = 16; base < WG; base += 16) {
-    __syncthreads();
-    if (threadIdx.x >= (unsigned)base && threadIdx.x < (unsigned)base + 16)
-      buf[threadIdx.x - base] = acc;
-    __syncthreads();
-    if (threadIdx.x < 16) fp12_mul_n(acc, acc, buf[threadIdx.x]);
-  }
-  for (int w = 8; w > 0; w >>= 1) {
+  for (int w = WGR / 2; w > 0; w >>= 1) {
     __syncthreads();
     if (threadIdx.x >= (unsigned)w && threadIdx.x < (unsigned)2 * w) buf[threadIdx.x - w] = acc;
     __syncthreads();
-    if (threadIdx.x < (unsigned)w) fp12_mul_n(acc, acc, buf[threadIdx.x]);
+    if (threadIdx.x < (unsigned)w) {
+      fp12 o = buf[threadIdx.x];
+      fp12_mul(acc, acc, o);
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    F[s] = acc;
+    part[s] = acc;
     err[s] = e_sh | (off[s + 1] == off[s] ? 1 : 0);
   }
 }
 
-// partial_s = F_s * MillerLoop(-g1, S_s)   (the segment's own e(-g1, sum r sig) term)
-__global__ void __launch_bounds__(WG) k_seg_partial(const fp12 *F, const g2j *S, uint32_t nseg,
-                                                    fp12 *part) {
-  uint32_t s = gtid();
-  if (s >= nseg) return;
-  g2a sa;
-  jac_to_aff(sa, S[s]);
-  g1a ng1;
-  fp_set(ng1.x, k::G1X_M);
-  fp_set(ng1.y, k::G1NEGY_M);
-  fp12 m;
-  miller_loop(m, ng1, sa);
-  fp12 r;
-  fp12_mul_n(r, F[s], m);
-  part[s] = r;
-}
-
-// verdict_s = FE(prod_k partial[k][s]) == 1 and no segment error on any part
-__global__ void __launch_bounds__(WG) k_final_verify(const fp12 *part, const int32_t *err,
-                                                     uint32_t nparts, uint32_t nseg,
-                                                     int32_t *verdict) {
+// ---------------------------------------------------------------- final exponentiation
+// product of nparts partials per segment (multi-GPU all-gather layout [part][seg]) and
+// the easy part.
+__global__ void __launch_bounds__(WG) k_fe_easy(const fp12 *part, const int32_t *err,
+                                                uint32_t nparts, uint32_t nseg, fp12 *F,
+                                                int32_t *err_out) {
   uint32_t s = gtid();
   if (s >= nseg) return;
   fp12 acc = part[s];
   int32_t e = err[s];
   for (uint32_t k = 1; k < nparts; k++) {
-    fp12_mul_n(acc, acc, part[(size_t)k * nseg + s]);
+    fp12 o = part[(size_t)k * nseg + s];
+    fp12_mul(acc, acc, o);
     e |= err[(size_t)k * nseg + s];
   }
   fp12 r;
-  final_exp(r, acc);
-  verdict[s] = (!e && fp12_is_one(r)) ? ST_SUCCESS : ST_VERIFY_FAIL;
+  fe_easy(r, acc);
+  F[s] = r;
+  err_out[s] = e;
 }
-
-// ---------------------------------------------------------------- single-pair checks
-// f_i = ML(pk_i, H_i) * ML(-g1, sig_i) with blst's pre-checks (a6/a7):
-// infinite pk -> fail; sig must be in G2 (sig_groupcheck = true); infinite sig skipped.
-__global__ void __launch_bounds__(WG) k_av_miller(const g2a *sigs, const g1a *pks, const g2a *H,
-                                                  const int32_t *pre, uint32_t m, fp12 *f,
-                                                  int32_t *bad) {
-  uint32_t i = gtid();
-  if (i >= m) return;
-  g1a pk = pks[i];
-  g2a sig = sigs[i];
-  int32_t b = (pre && pre[i] != ST_SUCCESS) ? 1 : 0;
-  if (aff_is_inf(pk)) b = 1;
-  if (!aff_is_inf(sig) && !g2_in_group(sig)) b = 1;
-  fp12 r;
-  fp12_one(r);
-  if (!b) {
-    miller_loop(r, pk, H[i]);
-    if (!aff_is_inf(sig)) {
-      g1a ng1;
-      fp_set(ng1.x, k::G1X_M);
-      fp_set(ng1.y, k::G1NEGY_M);
-      fp12 t;
-      miller_loop(t, ng1, sig);
-      fp12_mul_n(r, r, t);
-    }
-  }
-  f[i] = r;
-  bad[i] = b;
+__global__ void __launch_bounds__(WG) k_fe_xm1(const fp12 *in, uint32_t nseg, fp12 *out) {
+  uint32_t s = gtid();
+  if (s >= nseg) return;
+  fp12 a = in[s], r;
+  fe_s_xm1(r, a);
+  out[s] = r;
+}
+__global__ void __launch_bounds__(WG) k_fe_xpp(const fp12 *in, uint32_t nseg, fp12 *out) {
+  uint32_t s = gtid();
+  if (s >= nseg) return;
+  fp12 a = in[s], r;
+  fe_s_xpp(r, a);
+  out[s] = r;
+}
+__global__ void __launch_bounds__(WG) k_fe_x(const fp12 *in, uint32_t nseg, fp12 *out) {
+  uint32_t s = gtid();
+  if (s >= nseg) return;
+  fp12 a = in[s], r;
+  fp12_cyc_exp_x(r, a);
+  out[s] = r;
+}
+__global__ void __launch_bounds__(WG) k_fe_s5(const fp12 *T, const fp12 *B, uint32_t nseg,
+                                              fp12 *out) {
+  uint32_t s = gtid();
+  if (s >= nseg) return;
+  fp12 t = T[s], b = B[s], r;
+  fe_s5(r, t, b);
+  out[s] = r;
+}
+__global__ void __launch_bounds__(WG) k_fe_s6(const fp12 *C, const fp12 *F, const int32_t *err,
+                                              uint32_t nseg, int32_t *verdict) {
+  uint32_t s = gtid();
+  if (s >= nseg) return;
+  fp12 c = C[s], f = F[s], r;
+  fe_s6(r, c, f);
+  verdict[s] = (!err[s] && fp12_is_one(r)) ? ST_SUCCESS : ST_VERIFY_FAIL;
 }
 
 // ---------------------------------------------------------------- key material (a15)
@@ -348,8 +410,7 @@ __global__ void __launch_bounds__(WG) k_sign(const uint8_t *sks, const g2a *H, u
 }
 
 // ---------------------------------------------------------------- roofline probe
-// 8 independent v_mad_u64_u32 chains per lane; returns nothing useful, the timing is
-// the measurement (2 * iters * 8 mads per lane).
+// 8 independent v_mad_u64_u32 chains per lane (2 * iters * 8 mads per lane)
 __global__ void __launch_bounds__(256) k_mad_peak(uint64_t *sink, uint32_t iters, uint32_t seed) {
   uint32_t a = seed ^ threadIdx.x, b = seed * 2654435761u + blockIdx.x;
   uint64_t acc[8];

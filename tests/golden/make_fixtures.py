@@ -1,0 +1,305 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.json + trusted_setup.bin (committed fixtures).
+
+Inputs come from three places, each recorded in the fixture's "provenance":
+  * "reference": data held by the reference's own tests/assets -- interop keygen KATs
+    (/root/reference/interop/src/lib.rs:119-178), the EIP-2335 keypair
+    (eip_2335/src/lib.rs:505,552) and the KZG trusted setup
+    (kzg_utils/src/trusted_setup.txt, read here once and stored as trusted_setup.bin);
+  * "recalled": published vectors recalled from memory (RFC 9380 J.10.1 and
+    consensus-spec-tests bls/sign) -- accepted because the oracle reproduces them
+    bit-for-bit;
+  * "oracle": verdicts/points computed by oracle/bls12_381.py (pure-Python
+    restatement of blst semantics) on seeded synthetic inputs.
+Run from the repo root:  python tests/golden/make_fixtures.py
+"""
+
+import hashlib
+import json
+import os
+import random
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import bls12_381 as O  # noqa: E402
+
+REF_TS = "/root/reference/kzg_utils/src/trusted_setup.txt"
+
+INTEROP_KATS = [  # interop/src/lib.rs:123-160 (sk, pk) for validator indices 0..9
+    ("25295f0d1d592a90b333e26e85149708208e9f8e8bc18f6c77bd62f8ad7a6866",
+     "a99a76ed7796f7be22d5b7e85deeb7c5677e88e511e0b337618f8c4eb61349b4bf2d153f649f7b53359fe8b94a38e44c"),
+    ("51d0b65185db6989ab0b560d6deed19c7ead0e24b9b6372cbecb1f26bdfad000",
+     "b89bebc699769726a318c8e9971bd3171297c61aea4a6578a7a4f94b547dcba5bac16a89108b6b6a1fe3695d1a874a0b"),
+    ("315ed405fafe339603932eebe8dbfd650ce5dafa561f6928664c75db85f97857",
+     "a3a32b0f8b4ddb83f1a0a853d81dd725dfe577d4f4c3db8ece52ce2b026eca84815c1a7e8e92a4de3d755733bf7e4a9b"),
+    ("25b1166a43c109cb330af8945d364722757c65ed2bfed5444b5a2f057f82d391",
+     "88c141df77cd9d8d7a71a75c826c41a9c9f03c6ee1b180f3e7852f6a280099ded351b58d66e653af8e42816a4d8f532e"),
+    ("3f5615898238c4c4f906b507ee917e9ea1bb69b93f1dbd11a34d229c3b06784b",
+     "81283b7a20e1ca460ebd9bbd77005d557370cabb1f9a44f530c4c4c66230f675f8df8b4c2818851aa7d77a80ca5a4a5e"),
+    ("055794614bc85ed5436c1f5cab586aab6ca84835788621091f4f3b813761e7a8",
+     "ab0bdda0f85f842f431beaccf1250bf1fd7ba51b4100fd64364b6401fda85bb0069b3e715b58819684e7fc0b10a72a34"),
+    ("1023c68852075965e0f7352dee3f76a84a83e7582c181c10179936c6d6348893",
+     "9977f1c8b731a8d5558146bfb86caea26434f3c5878b589bf280a42c9159e700e9df0e4086296c20b011d2e78c27d373"),
+    ("3a941600dc41e5d20e818473b817a28507c23cdfdb4b659c15461ee5c71e41f5",
+     "a8d4c7c27795a725961317ef5953a7032ed6d83739db8b0e8a72353d1b8b4439427f7efa2c89caa03cc9f28f8cbab8ac"),
+    ("066e3bdc0415530e5c7fed6382d5c822c192b620203cf669903e1810a8c67d06",
+     "a6d310dbbfab9a22450f59993f87a4ce5db6223f3b5f1f30d2c4ec718922d400e0b3c7741de8e59960f72411a0ee10a7"),
+    ("2b3b88a041168a1c4cd04bdd8de7964fd35238f95442dc678514f9dadb81ec34",
+     "9893413c00283a3f9ed9fd9845dda1cea38228d22567f9541dccc357e54a2d6a6e204103c92564cbc05f4905ac7c493a"),
+]
+EIP2335 = ("000000000019d6689c085ae165831e934ff763ae46a2a6c172b3f1b60a8ce26f",
+           "9612d7a727c9d0a22e185a1c768478dfe919cada9266988cb32359c11f2b7b27f4ae4040902382ae2910c15e2b420d07")
+# web3signer test vectors (signer/src/web3signer/api.rs:116-124): decode-only points
+W3S_PKS = ["93247f2209abcacf57b75a51dafae777f9dd38bc7053d1af526f220a7489a6d3a2753e5f3e8b1cfe39b56f43611df74a",
+           "b53d21a4cfd562c469cc81514d4ce5a6b577d8403d32a394dc265dd190b47fa9f829fdd7963afdf972e5e77854051f6f"]
+W3S_SIG = ("b3baa751d0a9132cfe93e4e3d5ff9075111100e3789dca219ade5a24d27e19d16b3353149da1833e9b691bb3"
+           "8634e8dc04469be7032132906c927d7e1a49b414730612877bc6b2810c8f202daf793d1ab0d6b5cb21d52f9e52e883859887a5d9")
+
+RFC_DST = b"QUUX-V01-CS02-with-BLS12381G2_XMD:SHA-256_SSWU_RO_"
+RFC_VECTORS = [  # RFC 9380 Appendix J.10.1 (recalled): msg, P.x (c0, c1), P.y (c0, c1)
+    (b"", ("0141ebfbdca40eb85b87142e130ab689c673cf60f1a3e98d69335266f30d9b8d4ac44c1038e9dcdd5393faf5c41fb78a",
+           "05cb8437535e20ecffaef7752baddf98034139c38452458baeefab379ba13dff5bf5dd71b72418717047f5b0f37da03d"),
+     ("0503921d7f6a12805e72940b963c0cf3471c7b2a524950ca195d11062ee75ec076daf2d4bc358c4b190c0c98064fdd92",
+      "12424ac32561493f3fe3c260708a12b7c620e7be00099a974e259ddc7d1f6395c3c811cdd19f1e8dbf3e9ecfdcbab8d6")),
+    (b"abc", ("02c2d18e033b960562aae3cab37a27ce00d80ccd5ba4b7fe0e7a210245129dbec7780ccc7954725f4168aff2787776e6",
+              "139cddbccdc5e91b9623efd38c49f81a6f83f175e80b06fc374de9eb4b41dfe4ca3a230ed250fbe3a2acf73a41177fd8"),
+     ("1787327b68159716a37440985269cf584bcb1e621d3a7202be6ea05c4cfe244aeb197642555a0645fb87bf7466b2ba48",
+      "00aa65dae3c8d732d10ecd2c50f8a1baf3001578f71c694e03866e9f3d49ac1e1ce70dd94a733534f106d4cec0eddd16")),
+]
+ETH_SIGN_VECTORS = [  # consensus-spec-tests general/phase0/bls/sign (recalled)
+    ("263dbd792f5b1be47ed85f8938c0f29586af0d3ac7b977f21c278fe1462040e3", "00" * 32,
+     "b6ed936746e01f8ecf281f020953fbf1f01debd5657c4a383940b020b26507f6076334f91e2366c96e9ab279fb5158090352ea1c5b0c9274504f4f0e7053af24802e51e4568d164fe986834f41e55c8e850ce1f98458c0cfc9ab380b55285a55"),
+    ("47b8192d77bf871b62e87859d653922725724a5c031afeabc60bcef5ff665138", "00" * 32,
+     "b23c46be3a001c63ca711f87a005c200cc550b9429d5f4eb38d74322144f1b63926da3388979e5321012fb1a0526bcd100b5ef5fe72628ce4cd5e904aeaa3279527843fae5ca9ca675f4f51ed8f83bbf7155da9ecc9663100a885d5dc6df96d9"),
+    ("328388aff0d4a5b7dc9205abd374e7e98f3cd9f3418edb4eafda5fb16473d216", "00" * 32,
+     "948a7cb99f76d616c2c564ce9bf4a519f1bea6b0a624a02276443c245854219fabb8d4ce061d255af5330b078d5380681751aa7053da2c98bae898edc218c75f07e24d8802a17cd1f6833b71e58f5eb5b94208b4d0bb3848cecb075ea21be115"),
+]
+
+
+def h(b: bytes) -> str:
+    return b.hex()
+
+
+def e2_point_not_in_g2(rng):
+    """A point on E2 outside G2 (random x, no cofactor clearing)."""
+    while True:
+        x = (rng.randrange(O.P), rng.randrange(O.P))
+        y = O.f2_sqrt(O.f2_add(O.f2_mul(O.f2_sqr(x), x), O.B2))
+        if y is not None:
+            pt = (x, y)
+            if not O.g2_in_group(pt):
+                return pt
+
+
+def e1_point_not_in_g1(rng):
+    while True:
+        x = rng.randrange(O.P)
+        y = O.fp_sqrt(x * x * x + 4)
+        if y is not None and not O.g1_in_group((x, y)):
+            return (x, y)
+
+
+def main():
+    rng = random.Random(20251015)
+    out = {}
+
+    # -- keys ------------------------------------------------------------------------
+    kats = []
+    for i, (sk, pk) in enumerate(INTEROP_KATS):
+        assert O.interop_secret_key(i) == int(sk, 16)
+        assert O.g1_compress(O.sk_to_pk(int(sk, 16))).hex() == pk
+        kats.append({"index": i, "sk": sk, "pk": pk})
+    assert O.g1_compress(O.sk_to_pk(int(EIP2335[0], 16))).hex() == EIP2335[1]
+    out["keys"] = {"provenance": "reference: interop/src/lib.rs:119-178, eip_2335/src/lib.rs:505,552",
+                   "interop": kats, "eip2335": {"sk": EIP2335[0], "pk": EIP2335[1]}}
+
+    # -- hash_to_G2 and sign -------------------------------------------------------------
+    h2c = []
+    for msg, x, y in RFC_VECTORS:
+        pt = O.hash_to_g2(msg, RFC_DST)
+        assert pt == ((int(x[0], 16), int(x[1], 16)), (int(y[0], 16), int(y[1], 16)))
+        h2c.append({"msg": h(msg), "dst": h(RFC_DST), "x": list(x), "y": list(y)})
+    # POP-DST points from the oracle (the hot-path DST)
+    for j in range(4):
+        msg = hashlib.sha256(b"h2c%d" % j).digest()
+        (x0, x1), (y0, y1) = O.hash_to_g2(msg)
+        h2c.append({"msg": h(msg), "dst": h(O.DST_POP), "x": ["%096x" % x0, "%096x" % x1],
+                    "y": ["%096x" % y0, "%096x" % y1], "provenance": "oracle"})
+    out["hash_to_g2"] = {"provenance": "recalled: RFC 9380 J.10.1 (reproduced by the oracle); oracle",
+                         "cases": h2c}
+    sign = []
+    for sk, msg, sig in ETH_SIGN_VECTORS:
+        assert O.g2_compress(O.sign(int(sk, 16), bytes.fromhex(msg))).hex() == sig
+        sign.append({"sk": sk, "msg": msg, "sig": sig})
+    out["sign"] = {"provenance": "recalled: consensus-spec-tests bls/sign (reproduced by the oracle)",
+                   "cases": sign}
+
+    # -- decode / encode edge cases ---------------------------------------------------------
+    g1c = []
+    for _, pk in INTEROP_KATS[:4]:
+        g1c.append({"in": pk, "status": O.SUCCESS, "validate_status": O.SUCCESS, "out": pk})
+    for pk in W3S_PKS:
+        st, p = O.g1_decompress(bytes.fromhex(pk))
+        g1c.append({"in": pk, "status": st, "validate_status": O.public_key_from_bytes(bytes.fromhex(pk))[0],
+                    "out": O.g1_compress(p).hex() if st == O.SUCCESS else None})
+    inf = "c0" + "00" * 47
+    g1c.append({"in": inf, "status": O.SUCCESS, "validate_status": O.PK_IS_INFINITY, "out": inf})
+    g1c.append({"in": "00" * 48, "status": O.BAD_ENCODING, "validate_status": O.BAD_ENCODING, "out": None})
+    g1c.append({"in": "c0" + "00" * 46 + "01", "status": O.BAD_ENCODING, "validate_status": O.BAD_ENCODING, "out": None})
+    g1c.append({"in": "e0" + "00" * 47, "status": O.BAD_ENCODING, "validate_status": O.BAD_ENCODING, "out": None})
+    pbytes = bytearray(O.P.to_bytes(48, "big"))
+    pbytes[0] |= 0x80
+    g1c.append({"in": pbytes.hex(), "status": O.BAD_ENCODING, "validate_status": O.BAD_ENCODING, "out": None})
+    # x with no square root -> not on curve
+    x = 1
+    while O.fp_sqrt(x ** 3 + 4) is not None:
+        x += 1
+    b = bytearray(x.to_bytes(48, "big"))
+    b[0] |= 0x80
+    g1c.append({"in": b.hex(), "status": O.POINT_NOT_ON_CURVE, "validate_status": O.POINT_NOT_ON_CURVE, "out": None})
+    # on curve, not in G1
+    pt = e1_point_not_in_g1(rng)
+    enc = O.g1_compress(pt)
+    g1c.append({"in": enc.hex(), "status": O.SUCCESS, "validate_status": O.POINT_NOT_IN_GROUP, "out": enc.hex()})
+    # (0, +-2): order 3
+    g1c.append({"in": "80" + "00" * 47, "status": O.POINT_NOT_IN_GROUP, "validate_status": O.POINT_NOT_IN_GROUP,
+                "out": None})
+    out["g1_decode"] = {"provenance": "reference keys + oracle edge cases (blst POINTonE1_Uncompress_Z)", "cases": g1c}
+
+    g2c = []
+    for _, _, sig in ETH_SIGN_VECTORS:
+        g2c.append({"in": sig, "status": O.SUCCESS, "in_group": True, "out": sig})
+    st, p = O.g2_decompress(bytes.fromhex(W3S_SIG))
+    g2c.append({"in": W3S_SIG, "status": st, "in_group": bool(st == O.SUCCESS and O.g2_in_group(p)),
+                "out": O.g2_compress(p).hex() if st == O.SUCCESS else None})
+    inf2 = "c0" + "00" * 95
+    g2c.append({"in": inf2, "status": O.SUCCESS, "in_group": True, "out": inf2})
+    g2c.append({"in": "00" * 96, "status": O.BAD_ENCODING, "in_group": False, "out": None})
+    g2c.append({"in": "c0" + "00" * 94 + "01", "status": O.BAD_ENCODING, "in_group": False, "out": None})
+    bb = bytearray(96)
+    bb[0:48] = O.P.to_bytes(48, "big")
+    bb[0] |= 0x80
+    g2c.append({"in": bytes(bb).hex(), "status": O.BAD_ENCODING, "in_group": False, "out": None})
+    bb = bytearray(96)
+    bb[48:96] = O.P.to_bytes(48, "big")
+    bb[0] = 0x80
+    g2c.append({"in": bytes(bb).hex(), "status": O.BAD_ENCODING, "in_group": False, "out": None})
+    x = (1, 0)
+    while O.f2_sqrt(O.f2_add(O.f2_mul(O.f2_sqr(x), x), O.B2)) is not None:
+        x = (x[0] + 1, 0)
+    bb = bytearray(x[1].to_bytes(48, "big") + x[0].to_bytes(48, "big"))
+    bb[0] |= 0x80
+    g2c.append({"in": bytes(bb).hex(), "status": O.POINT_NOT_ON_CURVE, "in_group": False, "out": None})
+    pt = e2_point_not_in_g2(rng)
+    enc = O.g2_compress(pt)
+    g2c.append({"in": enc.hex(), "status": O.SUCCESS, "in_group": False, "out": enc.hex()})
+    out["g2_decode"] = {"provenance": "recalled spec vectors + oracle edge cases (blst POINTonE2_Uncompress_Z)",
+                        "cases": g2c}
+
+    # -- synthetic keys and signatures ------------------------------------------------------
+    nkeys = 12
+    sks = [O.interop_secret_key(i) for i in range(nkeys)]
+    pks = [O.sk_to_pk(k) for k in sks]
+    msgs = [hashlib.sha256(b"msg%d" % i).digest() for i in range(nkeys)]
+    sigs = [O.sign(k, m) for k, m in zip(sks, msgs)]
+
+    def g1hex(p):
+        return O.g1_compress(p).hex()
+
+    def g2hex(p):
+        return O.g2_compress(p).hex()
+
+    # -- aggregation --------------------------------------------------------------------------
+    agg = []
+    for lo, hi in [(0, 1), (0, 2), (0, 5), (3, 12)]:
+        st, a = O.aggregate_public_keys(pks[lo:hi])
+        agg.append({"pks": [g1hex(p) for p in pks[lo:hi]], "status": st, "out": g1hex(a)})
+    agg.append({"pks": [g1hex(pks[0]), g1hex(O.g1_neg(pks[0]))], "status": O.SUCCESS, "out": g1hex(None)})
+    agg.append({"pks": [], "status": O.AGGR_TYPE_MISMATCH, "out": None})
+    sagg = [{"sigs": [g2hex(s) for s in sigs[:k]], "out": g2hex(O.aggregate_signatures(sigs[:k]))}
+            for k in (1, 2, 6)]
+    out["aggregate"] = {"provenance": "oracle (PublicKey::aggregate / Signature::aggregate)",
+                        "g1": agg, "g2": sagg}
+
+    # -- verify ----------------------------------------------------------------------------------
+    bad_sig = e2_point_not_in_g2(rng)
+    ver = []
+
+    def vcase(sig, msg, pk, note):
+        ver.append({"sig": g2hex(sig), "msg": msg.hex(), "pk": g1hex(pk), "expect": O.verify(sig, msg, pk),
+                    "note": note})
+
+    vcase(sigs[0], msgs[0], pks[0], "valid")
+    vcase(sigs[1], msgs[1], pks[1], "valid")
+    vcase(sigs[0], msgs[1], pks[0], "wrong message")
+    vcase(sigs[0], msgs[0], pks[1], "wrong key")
+    vcase(None, msgs[0], pks[0], "infinite signature")
+    vcase(sigs[0], msgs[0], None, "infinite public key")
+    vcase(bad_sig, msgs[0], pks[0], "signature not in G2")
+    q = b"????????????????????????????????"  # bls/src/signature.rs:166-171 test key, msg "foo"
+    skq = int.from_bytes(q, "big")
+    vcase(O.sign(skq, b"foo"), b"foo", O.sk_to_pk(skq), "signature.rs test triple")
+    out["verify"] = {"provenance": "oracle (Signature::verify, signature.rs:47-60)", "cases": ver}
+
+    # -- fast_aggregate_verify -------------------------------------------------------------------
+    fav = []
+    m = msgs[5]
+    committee = list(range(4))
+    agg_sig = O.aggregate_signatures([O.sign(sks[i], m) for i in committee])
+
+    def fcase(sig, msg, keys, note):
+        fav.append({"sig": g2hex(sig), "msg": msg.hex(), "pks": [g1hex(k) for k in keys],
+                    "expect": O.fast_aggregate_verify(sig, msg, keys), "note": note})
+
+    fcase(agg_sig, m, [pks[i] for i in committee], "valid")
+    fcase(agg_sig, m, [pks[i] for i in committee[:3]], "missing key")
+    fcase(agg_sig, msgs[6], [pks[i] for i in committee], "wrong message")
+    fcase(agg_sig, m, [], "no keys")
+    fcase(None, m, [pks[0], O.g1_neg(pks[0])], "keys cancel to infinity")
+    fcase(sigs[2], msgs[2], [pks[2]], "single key")
+    out["fast_aggregate_verify"] = {"provenance": "oracle (Signature::fast_aggregate_verify, signature.rs:77-93)",
+                                    "cases": fav}
+
+    # -- multi_verify ------------------------------------------------------------------------------
+    mv = []
+
+    def mcase(idx, sig_over=None, pk_over=None, msg_over=None, note=""):
+        ms = [msgs[i] for i in idx]
+        ss = [sigs[i] for i in idx]
+        ps = [pks[i] for i in idx]
+        for d, src in ((sig_over or {}, ss), (pk_over or {}, ps), (msg_over or {}, ms)):
+            for k, v in d.items():
+                src[k] = v
+        rands = [rng.randrange(1, 1 << 64) for _ in idx]
+        mv.append({"msgs": [x.hex() for x in ms], "sigs": [g2hex(s) for s in ss], "pks": [g1hex(p) for p in ps],
+                   "rands": [str(r) for r in rands], "expect": O.multi_verify(ms, ss, ps, rands), "note": note})
+
+    mcase([0], note="one set")
+    mcase(list(range(6)), note="six sets")
+    mcase(list(range(6)), sig_over={3: sigs[4]}, note="one swapped signature")
+    mcase(list(range(6)), msg_over={2: msgs[9]}, note="one wrong message")
+    mcase(list(range(4)), pk_over={1: None}, note="infinite public key")
+    mcase([0, 1], sig_over={0: sigs[1], 1: sigs[0]}, note="signatures swapped between sets")
+    mcase([7, 7, 8], note="duplicate set")
+    out["multi_verify"] = {"provenance": "oracle (Signature::multi_verify, signature.rs:95-129; fixed scalars)",
+                           "cases": mv}
+
+    for name, obj in out.items():
+        with open(os.path.join(HERE, name + ".json"), "w") as fh:
+            json.dump(obj, fh, indent=1)
+
+    # -- trusted setup (reference asset) ------------------------------------------------------------
+    if os.path.exists(REF_TS):
+        lines = open(REF_TS).read().split()
+        n1, n2 = int(lines[0]), int(lines[1])
+        g1 = b"".join(bytes.fromhex(x) for x in lines[2:2 + n1])
+        g2 = b"".join(bytes.fromhex(x) for x in lines[2 + n1:2 + n1 + n2])
+        with open(os.path.join(HERE, "trusted_setup.bin"), "wb") as fh:
+            fh.write(n1.to_bytes(4, "little") + n2.to_bytes(4, "little") + g1 + g2)
+    print("fixtures written:", sorted(out))
+
+
+if __name__ == "__main__":
+    main()

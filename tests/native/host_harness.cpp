@@ -95,70 +95,78 @@ void h_sk_to_pk(const uint8_t *sk32, uint8_t *out96) {
   jac_to_aff(a, acc);
   std::memcpy(out96, &a, 96);
 }
-// k_av_miller + k_final_verify for one set
-int h_verify(const uint8_t *sig192, const uint8_t *msg, uint32_t len, const uint8_t *pk96) {
-  g2a sig;
-  g1a pk;
-  std::memcpy(&sig, sig192, 192);
-  std::memcpy(&pk, pk96, 96);
-  if (aff_is_inf(pk)) return ST_VERIFY_FAIL;
-  if (!aff_is_inf(sig) && !g2_in_group(sig)) return ST_VERIFY_FAIL;
-  g2j h;
-  hash_to_g2(h, msg, len, dst_ref{POP, 43});
-  g2a ha;
-  jac_to_aff(ha, h);
-  fp12 f, t;
-  miller_loop(f, pk, ha);
-  if (!aff_is_inf(sig)) {
+// Sequential emulation of the device pipeline (gbls_capi.hip pipeline_partials +
+// pipeline_final), stage by stage with the same per-lane functions as the kernels.
+static void pipeline(const uint8_t *msgs, const uint32_t *msg_off, const uint8_t *sigs192,
+                     const uint8_t *pks96, const uint64_t *rands, const int32_t *pre, uint32_t n,
+                     const uint32_t *seg_off, uint32_t nseg, int32_t *verdicts) {
+  for (uint32_t s = 0; s < nseg; s++) {
+    fp12 acc;
+    fp12_one(acc);
+    g2j S;
+    jac_set_inf(S);
+    int err = seg_off[s + 1] == seg_off[s];
+    for (uint32_t i = seg_off[s]; i < seg_off[s + 1]; i++) {
+      const uint8_t *m = msg_off ? msgs + msg_off[i] : msgs + 32 * i;
+      uint32_t len = msg_off ? msg_off[i + 1] - msg_off[i] : 32;
+      fp2 u[2];
+      hash_to_field_g2(u, m, len, dst_ref{POP, 43});                       // k_h2c_field
+      g2j q0, q1, h;
+      map_to_g2(q0, u[0]);                                                // k_h2c_map
+      map_to_g2(q1, u[1]);
+      jac_add(q0, q0, q1);                                                // k_h2c_clear
+      clear_cofactor_g2(h, q0);
+      g2h H;
+      g2h_from_jac(H, h);
+      g1a pk;
+      g2a sig;
+      std::memcpy(&pk, pks96 + 96 * i, 96);
+      std::memcpy(&sig, sigs192 + 192 * i, 192);
+      uint64_t r = rands ? rands[i] : 1;
+      g1j t;                                                              // k_mv_g1mul
+      mul_u64(t, pk, r);
+      g1p P;
+      g1p_from_jac(P, t);
+      err |= aff_is_inf(pk) || (pre && pre[i]);
+      g2j R;                                                              // k_mv_g2mul
+      mul_u64(R, sig, r);
+      jac_add(S, S, R);                                                   // k_seg_g2_sum
+      fp12 f;
+      miller_loop(f, P, H);                                               // k_miller
+      fp12_mul(acc, acc, f);                                              // k_seg_fp12_prod
+    }
     g1a ng1;
     fp_set(ng1.x, k::G1X_M);
     fp_set(ng1.y, k::G1NEGY_M);
-    miller_loop(t, ng1, sig);
-    fp12_mul(f, f, t);
+    g1p PP;
+    g1p_from_aff(PP, ng1);
+    g2h QQ;
+    g2h_from_jac(QQ, S);
+    fp12 f;
+    miller_loop(f, PP, QQ);
+    fp12_mul(acc, acc, f);
+    fp12 r;
+    final_exp(r, acc);                                                    // k_fe_*
+    verdicts[s] = (!err && fp12_is_one(r)) ? ST_SUCCESS : ST_VERIFY_FAIL;
   }
-  fp12 r;
-  final_exp(r, f);
-  return fp12_is_one(r) ? ST_SUCCESS : ST_VERIFY_FAIL;
 }
-// the multi_verify stage sequence (k_hash_to_g2, k_mv_g1mul, k_mv_g2mul, k_seg_g2_sum,
-// k_miller, k_seg_fp12_prod, k_seg_partial, k_final_verify) for one segment
+
+// gbls_verify: sig subgroup check + single-set segment with r = 1
+int h_verify(const uint8_t *sig192, const uint8_t *msg, uint32_t len, const uint8_t *pk96) {
+  g2a sig;
+  std::memcpy(&sig, sig192, 192);
+  int32_t pre = !(aff_is_inf(sig) || (g2_on_curve(sig) && g2_in_group(sig)));
+  uint32_t moff[2] = {0, len}, soff[2] = {0, 1};
+  int32_t v;
+  pipeline(msg, moff, sig192, pk96, nullptr, &pre, 1, soff, 1, &v);
+  return v;
+}
 int h_multi_verify(const uint8_t *msgs32, const uint8_t *sigs192, const uint8_t *pks96,
                    const uint64_t *rands, uint32_t n) {
-  fp12 F;
-  fp12_one(F);
-  g2j S;
-  jac_set_inf(S);
-  int bad = n == 0;
-  for (uint32_t i = 0; i < n; i++) {
-    g2a sig, H;
-    g1a pk, P;
-    std::memcpy(&sig, sigs192 + 192 * i, 192);
-    std::memcpy(&pk, pks96 + 96 * i, 96);
-    g2j h;
-    hash_to_g2(h, msgs32 + 32 * i, 32, dst_ref{POP, 43});
-    jac_to_aff(H, h);
-    g1j t;
-    mul_u64(t, pk, rands[i]);
-    jac_to_aff(P, t);
-    bad |= aff_is_inf(pk);
-    g2j R;
-    mul_u64(R, sig, rands[i]);
-    jac_add(S, S, R);
-    fp12 f;
-    miller_loop(f, P, H);
-    fp12_mul(F, F, f);
-  }
-  g2a sa;
-  jac_to_aff(sa, S);
-  g1a ng1;
-  fp_set(ng1.x, k::G1X_M);
-  fp_set(ng1.y, k::G1NEGY_M);
-  fp12 m;
-  miller_loop(m, ng1, sa);
-  fp12_mul(F, F, m);
-  fp12 r;
-  final_exp(r, F);
-  return (!bad && fp12_is_one(r)) ? ST_SUCCESS : ST_VERIFY_FAIL;
+  uint32_t soff[2] = {0, n};
+  int32_t v;
+  pipeline(msgs32, nullptr, sigs192, pks96, rands, nullptr, n, soff, 1, &v);
+  return v;
 }
 
 }  // extern "C"

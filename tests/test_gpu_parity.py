@@ -1,0 +1,275 @@
+"""On-device parity: every C-ABI entry point against the committed golden fixtures
+(tests/golden, pinned to the reference's KATs and the oracle) and, at full batch sizes,
+against size-independent properties.  Bit-exact for every byte / verdict.
+"""
+
+import ctypes
+import hashlib
+import json
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def gold(name):
+    with open(os.path.join(GOLD, name + ".json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def L():
+    from grandine_amd import _lib as G
+    return G.lib()
+
+
+@pytest.fixture(scope="module")
+def G():
+    from grandine_amd import _lib as G
+    return G
+
+
+@pytest.fixture(scope="module")
+def B():
+    from grandine_amd import bls
+    return bls
+
+
+def _pk(B, hexstr):
+    if hexstr == "c0" + "00" * 47:
+        return B.PublicKey.default()
+    st, raw = B.decompress_public_keys([bytes.fromhex(hexstr)], validate=False)[0]
+    assert st == 0
+    return B.PublicKey(raw)
+
+
+def _sig(B, hexstr):
+    return B.Signature.try_from(bytes.fromhex(hexstr))
+
+
+# ------------------------------------------------------------------ keys / encodings
+def test_interop_and_eip2335_keys(B):
+    k = gold("keys")
+    sks = [bytes.fromhex(c["sk"]) for c in k["interop"]] + [bytes.fromhex(k["eip2335"]["sk"])]
+    want = [c["pk"] for c in k["interop"]] + [k["eip2335"]["pk"]]
+    got = [p.to_bytes().hex() for p in B.public_keys_batch(sks)]
+    assert got == want
+
+
+def test_g1_decode_cases(L, G):
+    cases = gold("g1_decode")["cases"]
+    n = len(cases)
+    inb = G.buf(b"".join(bytes.fromhex(c["in"]) for c in cases))
+    for validate in (0, 1):
+        out = ctypes.create_string_buffer(96 * n)
+        st = G.i32_array(n)
+        G.check(L.gbls_g1_decompress(inb, n, validate, out, st), "decompress")
+        for i, c in enumerate(cases):
+            assert st[i] == (c["validate_status"] if validate else c["status"]), (i, c)
+        if not validate:
+            ok = [i for i, c in enumerate(cases) if c["status"] == 0]
+            enc = ctypes.create_string_buffer(48 * len(ok))
+            pts = G.buf(b"".join(out.raw[96 * i:96 * i + 96] for i in ok))
+            G.check(L.gbls_g1_compress(pts, len(ok), enc), "compress")
+            for j, i in enumerate(ok):
+                assert enc.raw[48 * j:48 * j + 48].hex() == cases[i]["out"]
+
+
+def test_g2_decode_cases(L, G):
+    cases = gold("g2_decode")["cases"]
+    n = len(cases)
+    out = ctypes.create_string_buffer(192 * n)
+    st = G.i32_array(n)
+    G.check(L.gbls_g2_decompress(G.buf(b"".join(bytes.fromhex(c["in"]) for c in cases)), n, out, st), "g2")
+    ok = [i for i, c in enumerate(cases) if c["status"] == 0]
+    for i, c in enumerate(cases):
+        assert st[i] == c["status"], (i, c)
+    pts = G.buf(b"".join(out.raw[192 * i:192 * i + 192] for i in ok))
+    enc = ctypes.create_string_buffer(96 * len(ok))
+    G.check(L.gbls_g2_compress(pts, len(ok), enc), "compress")
+    grp = G.i32_array(len(ok))
+    G.check(L.gbls_g2_validate(pts, len(ok), grp), "validate")
+    for j, i in enumerate(ok):
+        assert enc.raw[96 * j:96 * j + 96].hex() == cases[i]["out"]
+        assert (grp[j] == 0) == cases[i]["in_group"], (i, cases[i])
+
+
+def test_trusted_setup_points_decode_and_sum(L, G):
+    """kzg_utils/src/trusted_setup.txt: all points decode, re-encode byte-identical,
+    lie in their groups, and the 4096 G1 Lagrange points sum to the G1 generator."""
+    raw = open(os.path.join(GOLD, "trusted_setup.bin"), "rb").read()
+    n1 = int.from_bytes(raw[0:4], "little")
+    n2 = int.from_bytes(raw[4:8], "little")
+    g1 = raw[8:8 + 48 * n1]
+    g2 = raw[8 + 48 * n1:8 + 48 * n1 + 96 * n2]
+    out1 = ctypes.create_string_buffer(96 * n1)
+    st1 = G.i32_array(n1)
+    G.check(L.gbls_g1_decompress(G.buf(g1), n1, 1, out1, st1), "g1")
+    assert all(st1[i] == 0 for i in range(n1))
+    enc1 = ctypes.create_string_buffer(48 * n1)
+    G.check(L.gbls_g1_compress(out1, n1, enc1), "c1")
+    assert enc1.raw == g1
+    agg = ctypes.create_string_buffer(96)
+    assert L.gbls_g1_aggregate(out1, n1, agg) == 0
+    enc = ctypes.create_string_buffer(48)
+    G.check(L.gbls_g1_compress(agg, 1, enc), "c")
+    assert enc.raw.hex() == ("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb")
+    out2 = ctypes.create_string_buffer(192 * n2)
+    st2 = G.i32_array(n2)
+    G.check(L.gbls_g2_decompress(G.buf(g2), n2, out2, st2), "g2")
+    assert all(st2[i] == 0 for i in range(n2))
+    grp = G.i32_array(n2)
+    G.check(L.gbls_g2_validate(out2, n2, grp), "v")
+    assert all(grp[i] == 0 for i in range(n2))
+    enc2 = ctypes.create_string_buffer(96 * n2)
+    G.check(L.gbls_g2_compress(out2, n2, enc2), "c2")
+    assert enc2.raw == g2
+
+
+# ------------------------------------------------------------------ hash / sign
+def test_hash_to_g2_vectors(L, G):
+    from oracle import bls12_381 as O
+    cases = gold("hash_to_g2")["cases"]
+    for c in cases:
+        msg = bytes.fromhex(c["msg"])
+        dst = bytes.fromhex(c["dst"])
+        out = ctypes.create_string_buffer(192)
+        G.check(L.gbls_hash_to_g2(G.buf(msg), G.u32_array([0, len(msg)]), 1, dst, len(dst), out), "h2c")
+        rinv = pow(1 << 384, -1, O.P)
+        limbs = [int.from_bytes(out.raw[48 * k:48 * k + 48], "little") * rinv % O.P for k in range(4)]
+        assert ["%096x" % v for v in limbs] == [c["x"][0], c["x"][1], c["y"][0], c["y"][1]]
+
+
+def test_sign_vectors(B):
+    cases = gold("sign")["cases"]
+    sigs = B.sign_batch([bytes.fromhex(c["sk"]) for c in cases], [bytes.fromhex(c["msg"]) for c in cases])
+    assert [s.to_bytes().hex() for s in sigs] == [c["sig"] for c in cases]
+
+
+# ------------------------------------------------------------------ aggregation
+def test_aggregate_cases(B):
+    a = gold("aggregate")
+    for c in a["g1"]:
+        keys = [_pk(B, h) for h in c["pks"]]
+        if c["status"] != 0:
+            with pytest.raises(B.NoPublicKeysToAggregate):
+                B.PublicKey.aggregate_nonempty(keys)
+            continue
+        assert B.PublicKey.aggregate_nonempty(keys).to_bytes().hex() == c["out"]
+    for c in a["g2"]:
+        sigs = [_sig(B, h) for h in c["sigs"]]
+        acc = sigs[0]
+        for s in sigs[1:]:
+            acc = acc.aggregate(s)
+        assert acc.to_bytes().hex() == c["out"]
+
+
+def test_aggregate_segments_api(L, G, B):
+    a = gold("aggregate")["g1"]
+    keys, off = [], [0]
+    for c in a:
+        keys += [_pk(B, h).raw for h in c["pks"]]
+        off.append(len(keys))
+    n = len(a)
+    out = ctypes.create_string_buffer(96 * n)
+    st = G.i32_array(n)
+    G.check(L.gbls_g1_aggregate_segments(G.buf(b"".join(keys)), G.u32_array(off), n, out, st), "seg")
+    for i, c in enumerate(a):
+        assert st[i] == c["status"]
+        if c["status"] == 0:
+            assert B.PublicKey(out.raw[96 * i:96 * i + 96]).to_bytes().hex() == c["out"]
+
+
+# ------------------------------------------------------------------ verdicts
+def test_verify_cases(B):
+    for c in gold("verify")["cases"]:
+        sig = _sig(B, c["sig"])
+        assert sig.verify(bytes.fromhex(c["msg"]), _pk(B, c["pk"])) == c["expect"], c["note"]
+
+
+def test_aggregate_verify_batch_matches_single(L, G, B):
+    cases = gold("verify")["cases"]
+    m = len(cases)
+    msgs = [bytes.fromhex(c["msg"]) for c in cases]
+    off = [0]
+    for x in msgs:
+        off.append(off[-1] + len(x))
+    v = G.i32_array(m)
+    G.check(L.gbls_aggregate_verify_batch(G.buf(b"".join(_sig(B, c["sig"]).raw for c in cases)), G.buf(b"".join(msgs)),
+                                          G.u32_array(off), G.buf(b"".join(_pk(B, c["pk"]).raw for c in cases)), m, v),
+            "batch")
+    assert [v[i] == 0 for i in range(m)] == [c["expect"] for c in cases]
+
+
+def test_fast_aggregate_verify_cases(B):
+    for c in gold("fast_aggregate_verify")["cases"]:
+        sig = _sig(B, c["sig"])
+        keys = [_pk(B, h) for h in c["pks"]]
+        assert sig.fast_aggregate_verify(bytes.fromhex(c["msg"]), keys) == c["expect"], c["note"]
+
+
+def test_multi_verify_cases(B):
+    for c in gold("multi_verify")["cases"]:
+        msgs = [bytes.fromhex(h) for h in c["msgs"]]
+        sigs = [_sig(B, h) for h in c["sigs"]]
+        pks = [_pk(B, h) for h in c["pks"]]
+        rands = [int(r) for r in c["rands"]]
+        assert B.Signature.multi_verify(msgs, sigs, pks, rands) == c["expect"], c["note"]
+
+
+def test_multi_verify_segments_independent_verdicts(L, G, B):
+    cases = gold("multi_verify")["cases"]
+    msgs, sigs, pks, rands, off = [], [], [], [], [0]
+    for c in cases:
+        msgs += [bytes.fromhex(h) for h in c["msgs"]]
+        sigs += [_sig(B, h).raw for h in c["sigs"]]
+        pks += [_pk(B, h).raw for h in c["pks"]]
+        rands += [int(r) for r in c["rands"]]
+        off.append(len(msgs))
+    v = G.i32_array(len(cases))
+    G.check(L.gbls_multi_verify_segments(G.buf(b"".join(msgs)), G.buf(b"".join(sigs)), G.buf(b"".join(pks)),
+                                         G.u64_array(rands), len(msgs), G.u32_array(off), len(cases), v), "segs")
+    assert [v[i] == 0 for i in range(len(cases))] == [c["expect"] for c in cases]
+
+
+# ------------------------------------------------------------------ verifier mirror
+def test_multi_verifier_finish(B):
+    from grandine_amd import verifier as V
+    k = gold("keys")["interop"]
+    sks = [bytes.fromhex(c["sk"]) for c in k[:4]]
+    msgs = [hashlib.sha256(b"mv%d" % i).digest() for i in range(4)]
+    sigs = B.sign_batch(sks, msgs)
+    pks = B.public_keys_batch(sks)
+    mv = V.MultiVerifier()
+    for m, s, p in zip(msgs, sigs, pks):
+        mv.verify_singular(m, s.to_bytes(), B.CachedPublicKey(p.to_bytes()), V.SignatureKind.Block)
+    mv.finish()
+    mv.triples[1].message = msgs[2]
+    with pytest.raises(V.SignatureInvalid):
+        mv.finish()
+    V.MultiVerifier().finish()  # verifier.rs:446-449
+
+
+# ------------------------------------------------------------------ full-size properties
+def _workload(B, n, seed=b"c2"):
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    sks = [(int.from_bytes(hashlib.sha256(seed + b"sk%d" % i).digest(), "big") % R).to_bytes(32, "big")
+           for i in range(n)]
+    msgs = [hashlib.sha256(seed + b"m%d" % i).digest() for i in range(n)]
+    return sks, msgs, B.sign_batch(sks, msgs), B.public_keys_batch(sks)
+
+
+def test_c2_batch_4096_accept_and_reject(B):
+    n = 4096
+    sks, msgs, sigs, pks = _workload(B, n)
+    rands = [(i * 0x9E3779B97F4A7C15 + 7) % (1 << 64) or 1 for i in range(n)]
+    assert B.Signature.multi_verify(msgs, sigs, pks, rands)
+    bad = list(sigs)
+    bad[1234] = sigs[1235]
+    assert not B.Signature.multi_verify(msgs, bad, pks, rands)
+    badm = list(msgs)
+    badm[4095] = hashlib.sha256(b"other").digest()
+    assert not B.Signature.multi_verify(badm, sigs, pks, rands)

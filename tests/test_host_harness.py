@@ -1,0 +1,103 @@
+"""CPU: the engine's own device arithmetic (grandine_amd/csrc/*.h), compiled for the host
+by tests/native/host_harness.cpp, against the golden fixtures and the oracle."""
+import ctypes
+import json
+import os
+import subprocess
+
+import pytest
+
+from oracle import bls12_381 as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+SO = os.path.join(ROOT, "tests", "native", "_build", "libhost_harness.so")
+RINV = pow(1 << 384, -1, O.P)
+
+
+def gold(name):
+    with open(os.path.join(GOLD, name + ".json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def H():
+    src = os.path.join(ROOT, "tests", "native", "host_harness.cpp")
+    os.makedirs(os.path.dirname(SO), exist_ok=True)
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-D__HIP_PLATFORM_AMD__",
+                           "-I/opt/rocm/include", "-o", SO, src])
+    L = ctypes.CDLL(SO)
+    L.h_multi_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+    return L
+
+
+def fp_b(x):
+    return (x * (1 << 384) % O.P).to_bytes(48, "little")
+
+
+def g1_b(p):
+    return bytes(96) if p is None else fp_b(p[0]) + fp_b(p[1])
+
+
+def g2_b(p):
+    return bytes(192) if p is None else fp_b(p[0][0]) + fp_b(p[0][1]) + fp_b(p[1][0]) + fp_b(p[1][1])
+
+
+def test_fp_mul_random(H):
+    import random
+    rng = random.Random(1)
+    for _ in range(200):
+        a, b = rng.randrange(O.P), rng.randrange(O.P)
+        out = ctypes.create_string_buffer(48)
+        H.h_fp_mul(a.to_bytes(48, "little"), b.to_bytes(48, "little"), out)
+        assert int.from_bytes(out.raw, "little") == a * b * pow(1 << 384, -1, O.P) % O.P
+
+
+def test_g1_decode_fixtures(H):
+    for c in gold("g1_decode")["cases"]:
+        out = ctypes.create_string_buffer(96)
+        assert H.h_g1_decompress(bytes.fromhex(c["in"]), 0, out) == c["status"]
+        assert H.h_g1_decompress(bytes.fromhex(c["in"]), 1, out) == c["validate_status"]
+        if c["validate_status"] == 0:
+            enc = ctypes.create_string_buffer(48)
+            H.h_g1_compress(out, enc)
+            assert enc.raw.hex() == c["out"]
+
+
+def test_g2_decode_fixtures(H):
+    for c in gold("g2_decode")["cases"]:
+        out = ctypes.create_string_buffer(192)
+        assert H.h_g2_decompress(bytes.fromhex(c["in"]), out) == c["status"]
+        if c["status"] == 0:
+            enc = ctypes.create_string_buffer(96)
+            H.h_g2_compress(out, enc)
+            assert enc.raw.hex() == c["out"]
+            assert bool(H.h_g2_in_group(out)) == c["in_group"]
+
+
+def test_hash_to_g2_fixtures(H):
+    for c in gold("hash_to_g2")["cases"]:
+        m, d = bytes.fromhex(c["msg"]), bytes.fromhex(c["dst"])
+        out = ctypes.create_string_buffer(192)
+        H.h_hash_to_g2(m, len(m), d, len(d), out)
+        v = [int.from_bytes(out.raw[48 * k:48 * k + 48], "little") * RINV % O.P for k in range(4)]
+        assert ["%096x" % x for x in v] == c["x"] + c["y"]
+
+
+def test_verify_fixtures(H):
+    for c in gold("verify")["cases"]:
+        sig = O.g2_decompress(bytes.fromhex(c["sig"]))[1]
+        pk = O.g1_decompress(bytes.fromhex(c["pk"]))[1]
+        m = bytes.fromhex(c["msg"])
+        assert (H.h_verify(g2_b(sig), m, len(m), g1_b(pk)) == 0) == c["expect"], c["note"]
+
+
+def test_multi_verify_fixtures(H):
+    for c in gold("multi_verify")["cases"]:
+        n = len(c["msgs"])
+        sigs = b"".join(g2_b(O.g2_decompress(bytes.fromhex(h))[1]) for h in c["sigs"])
+        pks = b"".join(g1_b(O.g1_decompress(bytes.fromhex(h))[1]) for h in c["pks"])
+        rands = (ctypes.c_uint64 * n)(*[int(r) for r in c["rands"]])
+        msgs = b"".join(bytes.fromhex(h) for h in c["msgs"])
+        assert (H.h_multi_verify(msgs, sigs, pks, rands, n) == 0) == c["expect"], c["note"]
