@@ -53,6 +53,10 @@ EXPORTS = [
     "gbls_sign",
     "gbls_hash_to_g2",
     "gbls_measure_mad64_peak",
+    "gbls_profile",
+    "gbls_profile_read",
+    "gbls_profile_reset",
+    "gbls_stage_name",
 ]
 
 
@@ -105,6 +109,10 @@ def load_library():
                 "gbls_sign": (_c.c_int, [_vp, _vp, _vp, _sz, _vp]),
                 "gbls_hash_to_g2": (_c.c_int, [_vp, _vp, _sz, _vp, _sz, _vp]),
                 "gbls_measure_mad64_peak": (_c.c_double, []),
+                "gbls_profile": (_c.c_int, [_c.c_int]),
+                "gbls_profile_read": (_c.c_int, [_vp, _vp, _c.c_int]),
+                "gbls_profile_reset": (None, []),
+                "gbls_stage_name": (_c.c_char_p, [_c.c_int]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(lib, name)

@@ -78,134 +78,135 @@ HD void jac_neg(jac<F> &r, const jac<F> &a) {
   r.z = a.z;
 }
 
-// dbl-2009-l (a = 0): 2M + 5S
+// The formulas below are written in liveness order: every input coordinate is consumed
+// as early as possible, so that (with the field products kept in program order, see
+// tools/gen_fpmul.py) a G2 point operation needs few live Fp2 temporaries.
+
+// dbl-2009-l (a = 0): 2M + 5S.  r may alias p.
 template <class F>
 HD void jac_dbl(jac<F> &r, const jac<F> &p) {
-  F A, B, C, D, E, Fq, t;
+  F A, B, C, t;
+  f_mul(t, p.y, p.z);
   f_sqr(A, p.x);
   f_sqr(B, p.y);
-  f_sqr(C, B);
-  f_add(t, p.x, B);
-  f_sqr(t, t);
+  f_add(C, p.x, B);  // X + B
+  f_dbl(r.z, t);     // Z3 = 2YZ   (p.y, p.z dead)
+  f_sqr(t, C);       // (X + B)^2  (p.x dead)
+  f_sqr(C, B);       // C = B^2    (B dead)
   f_sub(t, t, A);
   f_sub(t, t, C);
-  f_dbl(D, t);
-  f_dbl(E, A);
-  f_add(E, E, A);
-  f_sqr(Fq, E);
-  F z3;
-  f_mul(z3, p.y, p.z);
-  f_dbl(r.z, z3);
-  f_sub(r.x, Fq, D);
-  f_sub(r.x, r.x, D);
-  f_sub(t, D, r.x);
-  f_mul(t, E, t);
+  f_dbl(B, t);       // D = 2((X+B)^2 - A - C)
+  f_dbl(t, A);
+  f_add(A, t, A);    // E = 3A
+  f_sqr(t, A);       // F = E^2
+  f_sub(t, t, B);
+  f_sub(r.x, t, B);  // X3 = F - 2D
+  f_sub(t, B, r.x);
+  f_mul(t, A, t);    // E (D - X3)
   f_dbl(C, C);
   f_dbl(C, C);
   f_dbl(C, C);
-  f_sub(r.y, t, C);
+  f_sub(r.y, t, C);  // Y3 = E (D - X3) - 8C
 }
 
-// add-2007-bl with the doubling / inverse / infinity cases handled
+// add-2007-bl, r = a + b.  r may alias a (NOT b): the degenerate cases (a == +-b)
+// recompute from b, so a's coordinates can be consumed early.
 template <class F>
-HD void jac_add(jac<F> &r, const jac<F> &p, const jac<F> &q) {
-  if (jac_is_inf(p)) {
-    r = q;
+HD void jac_add(jac<F> &r, const jac<F> &a, const jac<F> &b) {
+  if (jac_is_inf(b)) {
+    r = a;
     return;
   }
-  if (jac_is_inf(q)) {
-    r = p;
+  if (jac_is_inf(a)) {
+    r = b;
     return;
   }
-  F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t;
-  f_sqr(z1z1, p.z);
-  f_sqr(z2z2, q.z);
-  f_mul(u1, p.x, z2z2);
-  f_mul(u2, q.x, z1z1);
-  f_mul(s1, p.y, q.z);
+  F z1z1, z2z2, u1, u2, s1, s2, t;
+  f_sqr(z1z1, a.z);
+  f_sqr(z2z2, b.z);
+  f_mul(u1, a.x, z2z2);
+  f_mul(u2, b.x, z1z1);
+  f_mul(s1, a.y, b.z);
   f_mul(s1, s1, z2z2);
-  f_mul(s2, q.y, p.z);
+  f_mul(s2, b.y, a.z);
   f_mul(s2, s2, z1z1);
-  f_sub(h, u2, u1);
-  f_sub(rr, s2, s1);
-  if (f_is_zero(h)) {
-    if (f_is_zero(rr)) {
-      jac_dbl(r, p);
-    } else {
-      jac_set_inf(r);
-    }
-    return;
-  }
-  f_dbl(i, h);
-  f_sqr(i, i);
-  f_mul(j, h, i);
-  f_dbl(rr, rr);
-  f_mul(v, u1, i);
-  jac<F> o;
-  f_sqr(o.x, rr);
-  f_sub(o.x, o.x, j);
-  f_sub(o.x, o.x, v);
-  f_sub(o.x, o.x, v);
-  f_sub(t, v, o.x);
-  f_mul(t, rr, t);
-  f_mul(s1, s1, j);
-  f_dbl(s1, s1);
-  f_sub(o.y, t, s1);
-  f_add(t, p.z, q.z);
+  f_add(t, a.z, b.z);
   f_sqr(t, t);
   f_sub(t, t, z1z1);
-  f_sub(t, t, z2z2);
-  f_mul(o.z, t, h);
-  r = o;
+  f_sub(t, t, z2z2);  // 2 Z1 Z2            (z1z1, z2z2, a.* dead)
+  f_sub(u2, u2, u1);  // H
+  f_sub(s2, s2, s1);
+  f_dbl(s2, s2);      // r = 2 (S2 - S1)
+  if (f_is_zero(u2)) {
+    if (f_is_zero(s2))
+      jac_dbl(r, b);
+    else
+      jac_set_inf(r);
+    return;
+  }
+  f_mul(r.z, t, u2);  // Z3 = 2 Z1 Z2 H
+  f_dbl(t, u2);
+  f_sqr(t, t);        // I = (2H)^2
+  f_mul(u2, u2, t);   // J = H I
+  f_mul(u1, u1, t);   // V = U1 I
+  f_sqr(t, s2);
+  f_sub(t, t, u2);
+  f_sub(t, t, u1);
+  f_sub(r.x, t, u1);  // X3 = r^2 - J - 2V
+  f_sub(t, u1, r.x);
+  f_mul(t, s2, t);    // r (V - X3)
+  f_mul(s1, s1, u2);
+  f_dbl(s1, s1);      // 2 S1 J
+  f_sub(r.y, t, s1);
 }
 
-// madd-2007-bl: p Jacobian + q affine (q not infinity)
+// madd-2007-bl: r = a + b for b affine.  r may alias a.
 template <class F>
-HD void jac_add_aff(jac<F> &r, const jac<F> &p, const aff<F> &q) {
-  if (aff_is_inf(q)) {
-    r = p;
+HD void jac_add_aff(jac<F> &r, const jac<F> &a, const aff<F> &b) {
+  if (aff_is_inf(b)) {
+    r = a;
     return;
   }
-  if (jac_is_inf(p)) {
-    jac_from_aff(r, q);
+  if (jac_is_inf(a)) {
+    jac_from_aff(r, b);
     return;
   }
-  F z1z1, u2, s2, h, hh, i, j, rr, v, t;
-  f_sqr(z1z1, p.z);
-  f_mul(u2, q.x, z1z1);
-  f_mul(s2, q.y, p.z);
+  F z1z1, u2, s2, t, hh;
+  f_sqr(z1z1, a.z);
+  f_mul(u2, b.x, z1z1);
+  f_mul(s2, b.y, a.z);
   f_mul(s2, s2, z1z1);
-  f_sub(h, u2, p.x);
-  f_sub(rr, s2, p.y);
-  if (f_is_zero(h)) {
-    if (f_is_zero(rr)) {
-      jac_dbl(r, p);
+  f_sub(u2, u2, a.x);  // H
+  f_sub(s2, s2, a.y);
+  f_dbl(s2, s2);       // r = 2 (S2 - Y1)
+  if (f_is_zero(u2)) {
+    if (f_is_zero(s2)) {
+      jac<F> bj;
+      jac_from_aff(bj, b);
+      jac_dbl(r, bj);
     } else {
       jac_set_inf(r);
     }
     return;
   }
-  f_sqr(hh, h);
-  f_dbl(i, hh);
-  f_dbl(i, i);
-  f_mul(j, h, i);
-  f_dbl(rr, rr);
-  f_mul(v, p.x, i);
-  jac<F> o;
-  f_sqr(o.x, rr);
-  f_sub(o.x, o.x, j);
-  f_sub(o.x, o.x, v);
-  f_sub(o.x, o.x, v);
-  f_sub(t, v, o.x);
-  f_mul(t, rr, t);
-  f_mul(s2, p.y, j);
-  f_dbl(s2, s2);
-  f_sub(o.y, t, s2);
-  f_add(t, p.z, h);
+  f_add(t, a.z, u2);
   f_sqr(t, t);
+  f_sub(t, t, z1z1);   // (Z1 + H)^2 - Z1Z1        (z1z1 dead)
+  f_sqr(hh, u2);
+  f_sub(r.z, t, hh);   // Z3 = (Z1 + H)^2 - Z1Z1 - HH   (a.z dead)
+  f_dbl(hh, hh);
+  f_dbl(hh, hh);       // I = 4 HH
+  f_mul(z1z1, a.x, hh);  // V = X1 I
+  f_mul(hh, u2, hh);     // J = H I
+  f_mul(t, a.y, hh);
+  f_dbl(u2, t);          // 2 Y1 J                  (a.x, a.y dead)
+  f_sqr(t, s2);
+  f_sub(t, t, hh);
   f_sub(t, t, z1z1);
-  f_sub(o.z, t, hh);
-  r = o;
+  f_sub(r.x, t, z1z1);   // X3 = r^2 - J - 2V
+  f_sub(t, z1z1, r.x);
+  f_mul(t, s2, t);
+  f_sub(r.y, t, u2);     // Y3 = r (V - X3) - 2 Y1 J
 }
 
 template <class F>

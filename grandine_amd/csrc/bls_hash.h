@@ -28,7 +28,7 @@ HD void sha256_init(sha_state &s) {
   s.h[7] = 0x5be0cd19u;
 }
 
-HDNI void sha256_compress(sha_state &s, const uint32_t (&blk)[16]) {
+HD void sha256_compress(sha_state &s, const uint32_t (&blk)[16]) {
   const uint32_t K[64] = {
       0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
       0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
@@ -130,7 +130,7 @@ HD void sha_fill_block(uint32_t (&blk)[16], const b0_src &src, uint32_t base, ui
 }
 
 // expand_message_xmd(msg, DST, 256) -> 64 big-endian 32-bit words
-HDNI void expand_message_xmd_256(uint32_t (&out)[64], const uint8_t *msg, uint32_t mlen,
+HD void expand_message_xmd_256(uint32_t (&out)[64], const uint8_t *msg, uint32_t mlen,
                                  dst_ref dst) {
   sha_state s;
   sha256_init(s);
@@ -252,7 +252,8 @@ HD void map_to_curve_sswu(g2j &out, const fp2 &u) {
   fp_sqr(n, a1.c0);
   fp_sqr(nt, a1.c1);
   fp_add(n, n, nt);
-  fp_pow(gamma, n, k::EXP_SQRT);
+  fp_pow_pm3d4(gamma, n);
+  fp_mul(gamma, gamma, n);  // n^((p+1)/4)
   fp_sqr(g2, gamma);
   bool is_sq = fp_eq(g2, n);
   // x2 = Z u^2 x1, gx2 = (Z u^2)^3 gx1 -> U2 D = (Z u^2)^3 U D ; sqrt(N(.)) = N(u)^3 sqrt(-125) gamma
@@ -335,26 +336,27 @@ HD void iso_map_g2(g2j &out, const g2j &in) {
   fp2_mul(out.z, xd, yd);
 }
 
-// h_eff P = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P)   (RFC 9380 Appendix G.3 ordering)
+// h_eff P = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P)  (Budroni-Pintore; RFC 9380 G.3):
+//   t1 = [x]P;  t2 = [x](t1 + psi(P));  h = t2 - t1 + psi^2(2P) - psi(P) - P
+// ordered so that at most three Jacobian points are live at once.
 HD void clear_cofactor_g2(g2j &r, const g2j &p) {
-  g2j t1, t2, t3, negp;
+  g2j t1, t2, t3;
   mul_by_xabs(t1, p);
-  jac_neg(t1, t1);  // t1 = [x]P
-  g2_psi(t2, p);    // t2 = psi(P)
-  jac_dbl(t3, p);
-  g2_psi2(t3, t3);  // t3 = psi^2(2P)
-  g2j nt2;
-  jac_neg(nt2, t2);
-  jac_add(t3, t3, nt2);  // t3 - t2
-  jac_add(t2, t1, t2);   // t1 + t2
-  mul_by_xabs(t2, t2);
-  jac_neg(t2, t2);  // [x](t1 + t2)
-  jac_add(t3, t3, t2);
-  g2j nt1;
-  jac_neg(nt1, t1);
-  jac_add(t3, t3, nt1);
-  jac_neg(negp, p);
-  jac_add(r, t3, negp);
+  jac_neg(t1, t1);        // t1 = [x]P
+  g2_psi(t2, p);
+  jac_add(t2, t2, t1);    // t1 + psi(P)
+  mul_by_xabs(t3, t2);
+  jac_neg(t3, t3);        // t3 = [x](t1 + psi(P))
+  jac_neg(t1, t1);
+  jac_add(t3, t3, t1);    // - t1
+  jac_dbl(t1, p);
+  g2_psi2(t1, t1);
+  jac_add(t3, t3, t1);    // + psi^2(2P)
+  g2_psi(t1, p);
+  jac_neg(t1, t1);
+  jac_add(t3, t3, t1);    // - psi(P)
+  jac_neg(t1, p);
+  jac_add(r, t3, t1);     // - P
 }
 
 // hash_to_field (RFC 9380 §5.2, count = 2, m = 2, L = 64): msg -> u[0], u[1] in Fp2

@@ -1,0 +1,61 @@
+// Shared declarations of the engine's translation units.  Each k_*.hip file holds a
+// group of gfx950 kernels plus host launchers (declared here); gbls_capi.hip is the
+// host orchestration behind the C ABI.  Splitting the kernels over translation units
+// keeps every hipcc invocation small and lets the build run them in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "bls_hash.h"
+#include "bls_pairing.h"
+
+namespace gbls {
+
+constexpr int WG = 64;    // per-lane kernels: one wave per workgroup
+constexpr int WGR = 256;  // segment reductions: 4 waves, LDS tree
+constexpr uint32_t NONE = 0xffffffffu;
+
+inline unsigned nblk(size_t n, unsigned per = WG) { return (unsigned)((n + per - 1) / per); }
+
+// k_decode.hip -- encodings, aggregation, key material, roofline probe
+void launch_g1_decompress(hipStream_t st, const uint8_t *in, uint32_t n, int validate, g1a *out,
+                          int32_t *status);
+void launch_g2_decompress(hipStream_t st, const uint8_t *in, uint32_t n, g2a *out, int32_t *status);
+void launch_g2_check(hipStream_t st, const g2a *in, uint32_t n, int32_t *status, int accumulate);
+void launch_g1_compress(hipStream_t st, const g1a *in, uint32_t n, uint8_t *out);
+void launch_g2_compress(hipStream_t st, const g2a *in, uint32_t n, uint8_t *out);
+void launch_g1_aggregate_seg(hipStream_t st, const g1a *pks, const uint32_t *off, uint32_t nseg,
+                             g1a *out, int32_t *status);
+void launch_g2_aggregate_seg(hipStream_t st, const g2a *pts, const uint32_t *off, uint32_t nseg,
+                             g2a *out);
+void launch_sk_to_pk(hipStream_t st, const uint8_t *sks, uint32_t n, g1a *out);
+void launch_sign(hipStream_t st, const uint8_t *sks, const g2a *H, uint32_t n, g2a *out);
+void launch_mad_peak(hipStream_t st, unsigned blocks, uint64_t *sink, uint32_t iters, uint32_t seed);
+
+// k_h2c.hip -- hash_to_G2 stages
+void launch_h2c_field(hipStream_t st, const uint8_t *msg, const uint32_t *off, uint32_t n,
+                      const uint8_t *dst, uint32_t dlen, fp2 *U);
+void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q);
+void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H);
+
+// k_scalar.hip -- random-scalar products and the per-segment signature sum
+void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, const int32_t *pre,
+                     uint32_t n, g1a *P, int32_t *bad);
+void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R);
+void launch_seg_g2_sum(hipStream_t st, const g2j *R, const int32_t *bad, const uint32_t *seg_off,
+                       uint32_t nseg, uint32_t n, g1a *P, g2a *H, int32_t *seg_err);
+
+// k_lines.hip -- Miller-loop line functions of every pair
+void launch_lines(hipStream_t st, const g2a *H, uint32_t np, uint32_t *lines);
+
+// k_miller.hip -- Miller product tree + Horner
+void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1a *P,
+                    const uint32_t *couples, uint32_t ncouple, fp12 *V0);
+void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
+                      uint32_t nout, fp12 *Vout);
+void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial);
+
+// k_fexp.hip -- product of partials, final exponentiation, verdict
+void launch_final_verdict(hipStream_t st, const fp12 *partials, const int32_t *err,
+                          uint32_t nparts, uint32_t nseg, int32_t *verdict);
+
+}  // namespace gbls

@@ -1,0 +1,85 @@
+// gfx950 kernels: point encodings (a8, a9, a10) and the signature subgroup check,
+// one lane per point.
+
+#include "gbls_common.h"
+
+namespace gbls {
+
+__global__ void __launch_bounds__(WG) k_g1_decompress(const uint8_t *in, uint32_t n, int validate,
+                                                      g1a *out, int32_t *st) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g1a a;
+  int32_t s = g1_decompress(a, in + 48u * i);
+  if (s == ST_SUCCESS && validate) {  // PublicKey::validate, public_key.rs:27
+    if (aff_is_inf(a))
+      s = ST_PK_IS_INFINITY;
+    else if (!g1_in_group(a))
+      s = ST_NOT_IN_GROUP;
+  }
+  if (s != ST_SUCCESS) {
+    fp_zero(a.x);
+    fp_zero(a.y);
+  }
+  out[i] = a;
+  st[i] = s;
+}
+
+__global__ void __launch_bounds__(WG) k_g2_decompress(const uint8_t *in, uint32_t n, g2a *out,
+                                                      int32_t *st) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g2a a;
+  int32_t s = g2_decompress(a, in + 96u * i);
+  if (s != ST_SUCCESS) {
+    fp2_zero(a.x);
+    fp2_zero(a.y);
+  }
+  out[i] = a;
+  st[i] = s;
+}
+
+// signature subgroup check (sig_groupcheck = true in verify / fast_aggregate_verify,
+// signature.rs:51,86); infinity passes.  st[i] |= 1 on failure when `accumulate`.
+__global__ void __launch_bounds__(WG) k_g2_check(const g2a *in, uint32_t n, int32_t *st,
+                                                 int accumulate) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g2a a = in[i];
+  bool ok = aff_is_inf(a) || (g2_on_curve(a) && g2_in_group(a));
+  if (accumulate)
+    st[i] = st[i] | (ok ? 0 : 1);
+  else
+    st[i] = ok ? ST_SUCCESS : ST_NOT_IN_GROUP;
+}
+
+__global__ void __launch_bounds__(WG) k_g1_compress(const g1a *in, uint32_t n, uint8_t *out) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g1_compress(out + 48u * i, in[i]);
+}
+__global__ void __launch_bounds__(WG) k_g2_compress(const g2a *in, uint32_t n, uint8_t *out) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g2_compress(out + 96u * i, in[i]);
+}
+
+// ---------------------------------------------------------------- launchers
+void launch_g1_decompress(hipStream_t st, const uint8_t *in, uint32_t n, int validate, g1a *out,
+                          int32_t *status) {
+  k_g1_decompress<<<nblk(n), WG, 0, st>>>(in, n, validate, out, status);
+}
+void launch_g2_decompress(hipStream_t st, const uint8_t *in, uint32_t n, g2a *out, int32_t *status) {
+  k_g2_decompress<<<nblk(n), WG, 0, st>>>(in, n, out, status);
+}
+void launch_g2_check(hipStream_t st, const g2a *in, uint32_t n, int32_t *status, int accumulate) {
+  k_g2_check<<<nblk(n), WG, 0, st>>>(in, n, status, accumulate);
+}
+void launch_g1_compress(hipStream_t st, const g1a *in, uint32_t n, uint8_t *out) {
+  k_g1_compress<<<nblk(n), WG, 0, st>>>(in, n, out);
+}
+void launch_g2_compress(hipStream_t st, const g2a *in, uint32_t n, uint8_t *out) {
+  k_g2_compress<<<nblk(n), WG, 0, st>>>(in, n, out);
+}
+
+}  // namespace gbls

@@ -1,0 +1,140 @@
+// gfx950 kernels: segmented point aggregation (a4, a5, a11: one 256-lane workgroup per
+// segment), key material for fixtures (a15) and the v_mad_u64_u32 roofline probe.
+#include "gbls_common.h"
+
+namespace gbls {
+
+// Workgroup tree reduction of one Jacobian point per lane through LDS (result: lane 0)
+template <class F>
+__device__ void wg_reduce_jac(jac<F> &v) {
+  __shared__ jac<F> buf[WGR / 2];
+  for (int w = WGR / 2; w > 0; w >>= 1) {
+    __syncthreads();
+    if (threadIdx.x >= (unsigned)w && threadIdx.x < (unsigned)2 * w) buf[threadIdx.x - w] = v;
+    __syncthreads();
+    if (threadIdx.x < (unsigned)w) {
+      jac<F> o = buf[threadIdx.x];
+      jac_add(v, v, o);
+    }
+  }
+}
+
+// one workgroup per segment: pks[off[s] .. off[s+1]) -> affine sum (a4/a5)
+__global__ void __launch_bounds__(WGR) k_g1_aggregate_seg(const g1a *pks, const uint32_t *off,
+                                                          uint32_t nseg, g1a *out, int32_t *st) {
+  uint32_t s = blockIdx.x;
+  if (s >= nseg) return;
+  uint32_t b = off[s], e = off[s + 1];
+  g1j acc;
+  jac_set_inf(acc);
+  for (uint32_t i = b + threadIdx.x; i < e; i += WGR) jac_add_aff(acc, acc, pks[i]);
+  wg_reduce_jac(acc);
+  if (threadIdx.x == 0) {
+    g1a r;
+    jac_to_aff(r, acc);
+    out[s] = r;
+    st[s] = (e > b) ? ST_SUCCESS : ST_AGGR_TYPE_MISMATCH;
+  }
+}
+
+__global__ void __launch_bounds__(WGR) k_g2_aggregate_seg(const g2a *pts, const uint32_t *off,
+                                                          uint32_t nseg, g2a *out) {
+  uint32_t s = blockIdx.x;
+  if (s >= nseg) return;
+  uint32_t b = off[s], e = off[s + 1];
+  g2j acc;
+  jac_set_inf(acc);
+  for (uint32_t i = b + threadIdx.x; i < e; i += WGR) jac_add_aff(acc, acc, pts[i]);
+  wg_reduce_jac(acc);
+  if (threadIdx.x == 0) {
+    g2a r;
+    jac_to_aff(r, acc);
+    out[s] = r;
+  }
+}
+
+// ---------------------------------------------------------------- key material (a15)
+HD void scalar_from_be32(uint32_t (&s)[8], const uint8_t *b) {
+  for (int i = 0; i < 8; i++) {
+    const uint8_t *q = b + 4 * (7 - i);
+    s[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+template <class F>
+__device__ void mul_scalar256(jac<F> &r, const aff<F> &base, const uint32_t (&s)[8]) {
+  jac<F> acc;
+  jac_set_inf(acc);
+  for (int i = 255; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    if ((s[i >> 5] >> (i & 31)) & 1) jac_add_aff(acc, acc, base);
+  }
+  r = acc;
+}
+
+__global__ void __launch_bounds__(WG) k_sk_to_pk(const uint8_t *sks, uint32_t n, g1a *out) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s[8];
+  scalar_from_be32(s, sks + 32u * i);
+  g1a g;
+  fp_set(g.x, k::G1X_M);
+  fp_set(g.y, k::G1Y_M);
+  g1j t;
+  mul_scalar256(t, g, s);
+  g1a a;
+  jac_to_aff(a, t);
+  out[i] = a;
+}
+
+__global__ void __launch_bounds__(WG) k_sign(const uint8_t *sks, const g2a *H, uint32_t n,
+                                             g2a *out) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s[8];
+  scalar_from_be32(s, sks + 32u * i);
+  g2j t;
+  mul_scalar256(t, H[i], s);
+  g2a a;
+  jac_to_aff(a, t);
+  out[i] = a;
+}
+
+// ---------------------------------------------------------------- roofline probe
+// 8 independent v_mad_u64_u32 chains per lane (2 * iters * 8 mads per lane)
+__global__ void __launch_bounds__(256) k_mad_peak(uint64_t *sink, uint32_t iters, uint32_t seed) {
+  uint32_t a = seed ^ threadIdx.x, b = seed * 2654435761u + blockIdx.x;
+  uint64_t acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) acc[j] = (uint64_t)(a + j) << 7;
+  for (uint32_t it = 0; it < iters; it++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) acc[j] = (uint64_t)(uint32_t)acc[j] * b + acc[j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) acc[j] = (uint64_t)(uint32_t)(acc[j] >> 32) * a + acc[j];
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) x ^= acc[j];
+  if (x == 0x123456789ull) sink[0] = x;
+}
+
+// ---------------------------------------------------------------- launchers
+void launch_g1_aggregate_seg(hipStream_t st, const g1a *pks, const uint32_t *off, uint32_t nseg,
+                             g1a *out, int32_t *status) {
+  k_g1_aggregate_seg<<<nseg, WGR, 0, st>>>(pks, off, nseg, out, status);
+}
+void launch_g2_aggregate_seg(hipStream_t st, const g2a *pts, const uint32_t *off, uint32_t nseg,
+                             g2a *out) {
+  k_g2_aggregate_seg<<<nseg, WGR, 0, st>>>(pts, off, nseg, out);
+}
+void launch_sk_to_pk(hipStream_t st, const uint8_t *sks, uint32_t n, g1a *out) {
+  k_sk_to_pk<<<nblk(n), WG, 0, st>>>(sks, n, out);
+}
+void launch_sign(hipStream_t st, const uint8_t *sks, const g2a *H, uint32_t n, g2a *out) {
+  k_sign<<<nblk(n), WG, 0, st>>>(sks, H, n, out);
+}
+void launch_mad_peak(hipStream_t st, unsigned blocks, uint64_t *sink, uint32_t iters, uint32_t seed) {
+  k_mad_peak<<<blocks, 256, 0, st>>>(sink, iters, seed);
+}
+
+}  // namespace gbls

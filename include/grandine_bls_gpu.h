@@ -116,8 +116,10 @@ int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *
                                const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                const uint32_t *seg_off, size_t nseg, int32_t *verdicts);
 
-/* Device-pointer variants (all pointers are device memory; verdicts/partials too).
- * stream may be NULL (the library's own stream).  Asynchronous: the caller syncs. */
+/* Device-pointer variants: inputs, outputs, verdicts and partials are device memory
+ * (already resident in HBM); seg_off is a HOST array of nseg + 1 offsets (it sets the
+ * launch geometry).  stream may be NULL (the library's own stream).  Asynchronous:
+ * the caller synchronises the stream. */
 int gbls_multi_verify_segments_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
                                       const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                       const uint32_t *seg_off, size_t nseg, int32_t *verdicts,
@@ -142,6 +144,15 @@ int gbls_hash_to_g2(const uint8_t *msg_data, const uint32_t *msg_off, size_t n, 
 
 /* roofline helper: measured v_mad_u64_u32 throughput of this device (mad64/s) */
 double gbls_measure_mad64_peak(void);
+
+/* Per-stage timing for bench.py: when enabled, HIP events bracket every pipeline stage
+ * on the stream it is launched on.  gbls_profile_read() waits for recorded events,
+ * accumulates milliseconds / launch counts per stage (names: gbls_stage_name) and
+ * returns the number of stages. */
+int gbls_profile(int enable);
+int gbls_profile_read(double *ms, uint32_t *calls, int max_stages);
+void gbls_profile_reset(void);
+const char *gbls_stage_name(int stage);
 
 #ifdef __cplusplus
 }

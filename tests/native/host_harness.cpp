@@ -3,9 +3,11 @@
 // the gfx950 kernels run against the Python oracle.  Not part of the product: the
 // shipped library (libgrandine_bls.so) has no CPU path.
 #include <cstring>
+#include <vector>
 
 #include "../../grandine_amd/csrc/bls_hash.h"
 #include "../../grandine_amd/csrc/bls_pairing.h"
+#include "../../grandine_amd/csrc/bls_wave12.h"
 
 using namespace gbls;
 
@@ -95,59 +97,173 @@ void h_sk_to_pk(const uint8_t *sk32, uint8_t *out96) {
   jac_to_aff(a, acc);
   std::memcpy(out96, &a, 96);
 }
+// stage-by-stage hash_to_G2 intermediates (layout of tools/debug/h2c_dbg.hip's Out)
+struct H2cStages {
+  fp2 u[2];
+  g2j q[2];
+  g2j sum;
+  g2j h;
+  g2a ha;
+  fp sq_n, sq_gamma, inv_in, inv_out;
+};
+void h_h2c_stages(const uint8_t *msg, uint32_t len, const uint8_t *dst, uint32_t dlen, uint8_t *out) {
+  H2cStages o;
+  std::memset(&o, 0, sizeof o);
+  hash_to_field_g2(o.u, msg, len, dst_ref{dst, dlen});
+  map_to_g2(o.q[0], o.u[0]);
+  map_to_g2(o.q[1], o.u[1]);
+  g2j a = o.q[0];
+  jac_add(a, a, o.q[1]);
+  o.sum = a;
+  clear_cofactor_g2(o.h, a);
+  jac_to_aff(o.ha, o.h);
+  o.inv_in = o.u[0].c0;
+  fp_inv(o.inv_out, o.inv_in);
+  fp_pow_pm3d4(o.sq_gamma, o.u[0].c1);
+  std::memcpy(out, &o, sizeof o);
+}
+uint32_t h_h2c_stages_size() { return sizeof(H2cStages); }
+
+// ---- host emulation of the wave-cooperative Fp12 engine (bls_wave12.h): every round
+// runs lanes 0..63 in order, exactly as the single-wave device workgroup does.
+static void w12_mul_host(uint32_t *c, const uint32_t *a, const uint32_t *b) {
+  static uint32_t ws[W12_WS_WORDS];
+  for (int l = 0; l < 64; l++) w12_r_mul(l, a, b, ws);
+  for (int l = 0; l < 64; l++) w12_r_post1(l, ws);
+  for (int l = 0; l < 64; l++) w12_r_post2(l, ws);
+  for (int l = 0; l < 64; l++) w12_r_post3(l, ws, c);
+}
+static void w12_conj_host(uint32_t *c, const uint32_t *a) {
+  for (int l = 0; l < 64; l++) w12_r_conj(l, a, c);
+}
+static void w12_exp_x_host(uint32_t *c, const uint32_t *a) {
+  for (int l = 0; l < 64; l++) w12_r_copy(l, a, c);
+  for (int i = 62; i >= 0; i--) {
+    w12_mul_host(c, c, c);
+    if ((k::X_ABS >> i) & 1) w12_mul_host(c, c, a);
+  }
+  w12_conj_host(c, c);
+}
+// k_final_verdict's chain on the host engine emulation
+static bool w12_final_exp_is_one_host(const fp12 &f0) {
+  uint32_t f[144], F[144], A[144], B[144], T[144], X[144];
+  std::memcpy(f, &f0, sizeof f);
+  for (int l = 0; l < 64; l++) w12_r_inv(l, f, X);
+  w12_conj_host(A, f);
+  w12_mul_host(A, A, X);
+  for (int l = 0; l < 64; l++) w12_r_frob2(l, A, F);
+  w12_mul_host(F, F, A);
+  w12_exp_x_host(A, F);
+  w12_conj_host(X, F);
+  w12_mul_host(A, A, X);
+  w12_exp_x_host(B, A);
+  w12_conj_host(X, A);
+  w12_mul_host(A, B, X);
+  w12_exp_x_host(B, A);
+  for (int l = 0; l < 64; l++) w12_r_frob(l, A, X);
+  w12_mul_host(B, B, X);
+  w12_exp_x_host(T, B);
+  w12_exp_x_host(A, T);
+  for (int l = 0; l < 64; l++) w12_r_frob2(l, B, X);
+  w12_mul_host(A, A, X);
+  w12_conj_host(X, B);
+  w12_mul_host(A, A, X);
+  w12_mul_host(X, F, F);
+  w12_mul_host(X, X, F);
+  w12_mul_host(A, A, X);
+  return w12_is_one_image(A);
+}
+
+void h_fp12_mul_w12(const uint8_t *a576, const uint8_t *b576, uint8_t *out576) {
+  uint32_t a[144], b[144], c[144];
+  std::memcpy(a, a576, 576);
+  std::memcpy(b, b576, 576);
+  w12_mul_host(c, a, b);
+  std::memcpy(out576, c, 576);
+}
+void h_fp12_mul_ref(const uint8_t *a576, const uint8_t *b576, uint8_t *out576) {
+  fp12 a, b, c;
+  std::memcpy(&a, a576, 576);
+  std::memcpy(&b, b576, 576);
+  fp12_mul(c, a, b);
+  std::memcpy(out576, &c, 576);
+}
+int h_fp_inv_check(const uint8_t *a48, uint8_t *out48) {
+  fp a, r, t;
+  std::memcpy(a.l, a48, 48);
+  fp_inv(r, a);
+  std::memcpy(out48, r.l, 48);
+  fp_mul(t, r, a);
+  return fp_is_one(t);
+}
+
 // Sequential emulation of the device pipeline (gbls_capi.hip pipeline_partials +
-// pipeline_final), stage by stage with the same per-lane functions as the kernels.
+// pipeline_final): same per-lane functions, the Miller product over all pairs of a
+// segment formed event by event (as the device tree + Horner do), and the final
+// exponentiation on the emulated wave engine.
 static void pipeline(const uint8_t *msgs, const uint32_t *msg_off, const uint8_t *sigs192,
                      const uint8_t *pks96, const uint64_t *rands, const int32_t *pre, uint32_t n,
                      const uint32_t *seg_off, uint32_t nseg, int32_t *verdicts) {
   for (uint32_t s = 0; s < nseg; s++) {
-    fp12 acc;
-    fp12_one(acc);
+    uint32_t b = seg_off[s], e_ = seg_off[s + 1];
+    uint32_t np = e_ - b + 1;
+    std::vector<uint32_t> L((size_t)np * ML_EVENTS * 72);
+    std::vector<g1a> P(np);
     g2j S;
     jac_set_inf(S);
-    int err = seg_off[s + 1] == seg_off[s];
-    for (uint32_t i = seg_off[s]; i < seg_off[s + 1]; i++) {
+    int err = e_ == b;
+    for (uint32_t i = b; i < e_; i++) {
       const uint8_t *m = msg_off ? msgs + msg_off[i] : msgs + 32 * i;
       uint32_t len = msg_off ? msg_off[i + 1] - msg_off[i] : 32;
       fp2 u[2];
-      hash_to_field_g2(u, m, len, dst_ref{POP, 43});                       // k_h2c_field
+      hash_to_field_g2(u, m, len, dst_ref{POP, 43});  // k_h2c_field
       g2j q0, q1, h;
-      map_to_g2(q0, u[0]);                                                // k_h2c_map
+      map_to_g2(q0, u[0]);                            // k_h2c_map
       map_to_g2(q1, u[1]);
-      jac_add(q0, q0, q1);                                                // k_h2c_clear
+      jac_add(q0, q0, q1);                            // k_h2c_clear
       clear_cofactor_g2(h, q0);
-      g2h H;
-      g2h_from_jac(H, h);
+      g2a H;
+      jac_to_aff(H, h);
       g1a pk;
       g2a sig;
       std::memcpy(&pk, pks96 + 96 * i, 96);
       std::memcpy(&sig, sigs192 + 192 * i, 192);
       uint64_t r = rands ? rands[i] : 1;
-      g1j t;                                                              // k_mv_g1mul
+      g1j t;                                          // k_mv_g1mul
       mul_u64(t, pk, r);
-      g1p P;
-      g1p_from_jac(P, t);
+      jac_to_aff(P[i - b], t);
       err |= aff_is_inf(pk) || (pre && pre[i]);
-      g2j R;                                                              // k_mv_g2mul
+      g2j R;                                          // k_mv_g2mul
       mul_u64(R, sig, r);
-      jac_add(S, S, R);                                                   // k_seg_g2_sum
-      fp12 f;
-      miller_loop(f, P, H);                                               // k_miller
-      fp12_mul(acc, acc, f);                                              // k_seg_fp12_prod
+      jac_add(S, S, R);                               // k_seg_g2_sum
+      lines_of(L.data(), np, i - b, H);               // k_lines
     }
-    g1a ng1;
-    fp_set(ng1.x, k::G1X_M);
-    fp_set(ng1.y, k::G1NEGY_M);
-    g1p PP;
-    g1p_from_aff(PP, ng1);
-    g2h QQ;
-    g2h_from_jac(QQ, S);
+    fp_set(P[np - 1].x, k::G1X_M);
+    fp_set(P[np - 1].y, k::G1NEGY_M);
+    g2a Sa;
+    jac_to_aff(Sa, S);
+    lines_of(L.data(), np, np - 1, Sa);
+    // k_ml_leaf / k_ml_reduce / k_ml_horner
     fp12 f;
-    miller_loop(f, PP, QQ);
-    fp12_mul(acc, acc, f);
-    fp12 r;
-    final_exp(r, acc);                                                    // k_fe_*
-    verdicts[s] = (!err && fp12_is_one(r)) ? ST_SUCCESS : ST_VERIFY_FAIL;
+    for (int e = 0; e < ML_EVENTS; e++) {
+      fp12 M;
+      fp12_one(M);
+      for (uint32_t j = 0; j < np; j++) {
+        fp2 L0, L2, L3;
+        sp034 sp;
+        line_get(L.data(), np, j, e, L0, L2, L3);
+        line_eval(sp, L0, L2, L3, P[j]);
+        fp12_mul_034(M, M, sp);
+      }
+      if (e == 0) {
+        f = M;
+      } else {
+        if (ev_is_dbl(e)) fp12_sqr(f, f);
+        fp12_mul(f, f, M);
+      }
+    }
+    fp12_conj(f, f);
+    verdicts[s] = (!err && w12_final_exp_is_one_host(f)) ? ST_SUCCESS : ST_VERIFY_FAIL;
   }
 }
 

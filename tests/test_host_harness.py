@@ -54,6 +54,39 @@ def test_fp_mul_random(H):
         assert int.from_bytes(out.raw, "little") == a * b * pow(1 << 384, -1, O.P) % O.P
 
 
+def test_fp_inv_binary_gcd(H):
+    import random
+    rng = random.Random(2)
+    for a in [1, 2, O.P - 1, O.P - 2] + [rng.randrange(1, O.P) for _ in range(100)]:
+        out = ctypes.create_string_buffer(48)
+        assert H.h_fp_inv_check(a.to_bytes(48, "little"), out) == 1
+        # Montgomery: input aR -> output a^-1 R
+        want = pow(a * RINV % O.P, -1, O.P) * (1 << 384) % O.P
+        assert int.from_bytes(out.raw, "little") == want
+
+
+def test_wave12_product_matches_tower_product(H):
+    """The wave-cooperative Fp12 product (generated linear maps, 54 lanes) equals the
+    tower Karatsuba product, including on extreme coefficients (0, 1, p-1)."""
+    import random
+    rng = random.Random(3)
+    specials = [0, 1, O.P - 1]
+    for t in range(40):
+        if t < 3:
+            av = [specials[t]] * 12
+            bv = [specials[(t + 1) % 3]] * 12
+        else:
+            av = [rng.choice(specials) if rng.random() < 0.2 else rng.randrange(O.P) for _ in range(12)]
+            bv = [rng.choice(specials) if rng.random() < 0.2 else rng.randrange(O.P) for _ in range(12)]
+        a = b"".join(x.to_bytes(48, "little") for x in av)
+        b = b"".join(x.to_bytes(48, "little") for x in bv)
+        o1 = ctypes.create_string_buffer(576)
+        o2 = ctypes.create_string_buffer(576)
+        H.h_fp12_mul_w12(a, b, o1)
+        H.h_fp12_mul_ref(a, b, o2)
+        assert o1.raw == o2.raw
+
+
 def test_g1_decode_fixtures(H):
     for c in gold("g1_decode")["cases"]:
         out = ctypes.create_string_buffer(96)
