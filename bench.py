@@ -43,8 +43,9 @@ W_FPMUL = {
     "k_h2c_clear": 2360,     # per set: Q0+Q1, 2 x [|x|] (63 dbl + 5 add), 5 adds, psi
     "k_mv_g1mul": 1240,      # per set: 64-bit G1 double-and-add + affine
     "k_mv_g2mul": 3150,      # per set: 64-bit G2 double-and-add
-    "k_seg_g2_sum": 48,      # per set: one Jacobian G2 add
+    "k_g2sum": 48,           # per set: one Jacobian G2 add
     "k_lines": 1530,         # per pair: 63 doubling + 5 addition line steps
+    "k_lines_S": 1530,       # per segment: the (-g1, S) pair's lines
     "k_ml_leaf": 34 * 68 // 2,  # per pair: 68 events x (eval + half a sparse*sparse)
     "k_ml_reduce": 54 * 68 // 2,  # per pair: 68 events x ~1/2 dense product
     "k_ml_horner": 0,
@@ -199,7 +200,7 @@ def main():
     if dom:
         tot_ms, ncalls = stages[dom]
         avg_s = tot_ms / ncalls * 1e-3
-        units = n + 1 if dom in ("k_lines", "k_ml_leaf", "k_ml_reduce") else n
+        units = {"k_ml_leaf": n + 1, "k_ml_reduce": n + 1, "k_lines_S": 1}.get(dom, n)
         mads = units * W_FPMUL.get(dom, 0) * MAD_PER_FPMUL
         ach = mads / avg_s / 1e12
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4),

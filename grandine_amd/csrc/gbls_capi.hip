@@ -47,21 +47,23 @@ struct Buf {
 
 // ---- optional per-stage timing (HIP events on the launch stream), for bench.py
 enum Stage {
-  S_H2C_FIELD, S_H2C_MAP, S_H2C_CLEAR, S_G1MUL, S_G2MUL, S_G2SUM, S_LINES, S_ML_LEAF,
+  S_H2C_FIELD, S_H2C_MAP, S_H2C_CLEAR, S_G1MUL, S_G2MUL, S_G2SUM, S_LINES, S_LINES_S, S_ML_LEAF,
   S_ML_REDUCE, S_ML_HORNER, S_FINAL, S_COUNT
 };
-const char *kStageNames[S_COUNT] = {"k_h2c_field", "k_h2c_map",  "k_h2c_clear", "k_mv_g1mul",
-                                    "k_mv_g2mul",  "k_seg_g2_sum", "k_lines",   "k_ml_leaf",
-                                    "k_ml_reduce", "k_ml_horner", "k_final_verdict"};
+const char *kStageNames[S_COUNT] = {"k_h2c_field", "k_h2c_map",   "k_h2c_clear", "k_mv_g1mul",
+                                    "k_mv_g2mul",  "k_g2sum",      "k_lines",     "k_lines_S",
+                                    "k_ml_leaf",   "k_ml_reduce",  "k_ml_horner", "k_final_verdict"};
 
 struct Engine {
   std::mutex mu;
   bool ready = false;
   int device = -1;
   hipStream_t stream = nullptr;
+  hipStream_t side1 = nullptr, side2 = nullptr;  // fork/join streams of the pipeline
+  hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr;
   // workspaces
-  Buf in0, in1, in2, in3, in4, in5, in6, U, Q, H, P, R, bad, lines, V0, V1, tab, segoff, part, err,
-      out0, out1;
+  Buf in0, in1, in2, in3, in4, in5, in6, U, Q, H, P, R, gpart, lines, V0, V1, tab, segoff, part,
+      err, out0, out1;
   // profiling
   bool prof = false;
   struct Rec {
@@ -118,6 +120,11 @@ bool engine_init_locked(uint32_t device_mask) {
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return fail(GBLS_ERR_NO_DEVICE);
   HIPCHK(hipSetDevice(dev));
   HIPCHK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&g.side1, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&g.side2, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&g.ev_fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&g.ev_side1, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&g.ev_side2, hipEventDisableTiming));
   g.device = dev;
   g.ready = true;
   return true;
@@ -161,10 +168,10 @@ bool pipeline_partials(const uint8_t *msgs, const uint32_t *msg_off, const g2a *
                        const uint32_t *seg_off, size_t nseg, fp12 *partials, int32_t *seg_err,
                        hipStream_t st) {
   const size_t np = n + nseg;
-  // ---- host tables: couples (level 0) and the reduction levels
-  std::vector<uint32_t> tab;  // [couples (2 per couple)] [level tables (2 per output)]...
+  // ---- host tables, one upload: [couples][g2 chunks][seg_chunk][reduction levels]
+  std::vector<uint32_t> tab;
   std::vector<uint32_t> cnt(nseg);
-  for (size_t s = 0; s < nseg; s++) {
+  for (size_t s = 0; s < nseg; s++) {  // level-0 couples of each segment's pair list
     std::vector<uint32_t> list;
     for (uint32_t i = seg_off[s]; i < seg_off[s + 1]; i++) list.push_back(i);
     list.push_back((uint32_t)(n + s));
@@ -175,11 +182,32 @@ bool pipeline_partials(const uint8_t *msgs, const uint32_t *msg_off, const g2a *
     }
   }
   const size_t ncouple = tab.size() / 2;
+  const size_t chunk_off = tab.size();
+  const uint32_t CH = 4 * WGR;  // sets per level-1 G2-sum workgroup
+  std::vector<uint32_t> seg_chunk(nseg + 1, 0);
+  for (size_t s = 0; s < nseg; s++) {
+    seg_chunk[s] = (uint32_t)((tab.size() - chunk_off) / 4);
+    for (uint32_t h = 0; h < 2; h++) {
+      uint32_t b = seg_off[s], e = seg_off[s + 1];
+      do {
+        uint32_t ce = std::min<uint32_t>(e, b + CH);
+        tab.push_back((uint32_t)s);
+        tab.push_back(h);
+        tab.push_back(b);
+        tab.push_back(ce);
+        b = ce;
+      } while (b < e);
+    }
+  }
+  const size_t nchunks = (tab.size() - chunk_off) / 4;
+  seg_chunk[nseg] = (uint32_t)nchunks;
+  const size_t segchunk_off = tab.size();
+  tab.insert(tab.end(), seg_chunk.begin(), seg_chunk.end());
   struct Level {
     size_t tab_off, nin, nout;
   };
   std::vector<Level> levels;
-  size_t cur_n = ncouple, maxn_odd = 0;
+  size_t cur_n = ncouple;
   while (*std::max_element(cnt.begin(), cnt.end()) > 1) {
     Level L{tab.size(), cur_n, 0};
     size_t in_base = 0;
@@ -197,24 +225,47 @@ bool pipeline_partials(const uint8_t *msgs, const uint32_t *msg_off, const g2a *
     levels.push_back(L);
     cnt = next;
     cur_n = L.nout;
-    if (levels.size() & 1) maxn_odd = std::max(maxn_odd, L.nout);
   }
   // ---- workspaces
   const size_t line_words = (size_t)np * ML_EVENTS * 72;
-  size_t v1_n = 0;
-  for (size_t l = 0; l < levels.size(); l += 2) v1_n = std::max(v1_n, levels[l].nout);
-  size_t v0_n = ncouple;
-  for (size_t l = 1; l < levels.size(); l += 2) v0_n = std::max(v0_n, levels[l].nout);
+  size_t v1_n = 1, v0_n = ncouple;
+  for (size_t l = 0; l < levels.size(); l++)
+    (l & 1 ? v0_n : v1_n) = std::max(l & 1 ? v0_n : v1_n, levels[l].nout);
   if (!g.U.ensure(2 * n * sizeof(fp2)) || !g.Q.ensure(2 * n * sizeof(g2j)) ||
       !g.H.ensure(np * sizeof(g2a)) || !g.P.ensure(np * sizeof(g1a)) ||
-      !g.R.ensure(n * sizeof(g2j) + 16) || !g.bad.ensure(n * sizeof(int32_t) + 16) ||
+      !g.R.ensure(2 * n * sizeof(g2j) + 16) || !g.gpart.ensure(nchunks * (sizeof(g2j) + 4)) ||
       !g.lines.ensure(line_words * 4) || !g.V0.ensure(ML_EVENTS * v0_n * sizeof(fp12)) ||
-      !g.V1.ensure(ML_EVENTS * std::max<size_t>(v1_n, 1) * sizeof(fp12)))
+      !g.V1.ensure(ML_EVENTS * v1_n * sizeof(fp12)) || !g.segoff.ensure((nseg + 1) * 4))
     return fail(GBLS_ERR_HIP);
-  if (!upload(g.tab, tab.data(), tab.size(), st) || !upload(g.segoff, seg_off, nseg + 1, st))
-    return false;
-  (void)maxn_odd;
+  if (!upload(g.tab, tab.data(), tab.size(), st)) return false;
+  HIPCHK(hipMemcpyAsync(g.segoff.p, seg_off, (nseg + 1) * 4, hipMemcpyHostToDevice, st));
   const uint32_t N = (uint32_t)n, NP = (uint32_t)np, NS = (uint32_t)nseg;
+  const uint32_t *T = g.tab.as<uint32_t>();
+  g2j *gpart = g.gpart.as<g2j>();
+  int32_t *gpart_err = reinterpret_cast<int32_t *>(gpart + nchunks);
+  // ---- fork: side stream 1 = G1 scalar products, side stream 2 = G2 sum + its lines,
+  // main stream = hash_to_G2 + the sets' lines; join before the Miller tree.
+  HIPCHK(hipEventRecord(g.ev_fork, st));
+  HIPCHK(hipStreamWaitEvent(g.side1, g.ev_fork, 0));
+  HIPCHK(hipStreamWaitEvent(g.side2, g.ev_fork, 0));
+  {
+    StageTimer t(S_G1MUL, g.side1);
+    launch_mv_g1mul(g.side1, pks, rands, N, g.P.as<g1a>());
+  }
+  {
+    StageTimer t(S_G2MUL, g.side2);
+    launch_mv_g2mul(g.side2, sigs, rands, N, g.R.as<g2j>());
+  }
+  {
+    StageTimer t(S_G2SUM, g.side2);
+    launch_g2sum(g.side2, g.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
+                 g.segoff.as<uint32_t>(), NS, N, pks, pre, gpart, gpart_err, g.P.as<g1a>(),
+                 g.H.as<g2a>(), seg_err);
+  }
+  {
+    StageTimer t(S_LINES_S, g.side2);
+    launch_lines(g.side2, g.H.as<g2a>(), N, NS, NP, g.lines.as<uint32_t>());
+  }
   {
     StageTimer t(S_H2C_FIELD, st);
     launch_h2c_field(st, msgs, msg_off, N, nullptr, 0, g.U.as<fp2>());
@@ -228,33 +279,23 @@ bool pipeline_partials(const uint8_t *msgs, const uint32_t *msg_off, const g2a *
     launch_h2c_clear(st, g.Q.as<g2j>(), N, g.H.as<g2a>());
   }
   {
-    StageTimer t(S_G1MUL, st);
-    launch_mv_g1mul(st, pks, rands, pre, N, g.P.as<g1a>(), g.bad.as<int32_t>());
-  }
-  {
-    StageTimer t(S_G2MUL, st);
-    launch_mv_g2mul(st, sigs, rands, N, g.R.as<g2j>());
-  }
-  {
-    StageTimer t(S_G2SUM, st);
-    launch_seg_g2_sum(st, g.R.as<g2j>(), g.bad.as<int32_t>(), g.segoff.as<uint32_t>(), NS, N,
-                      g.P.as<g1a>(), g.H.as<g2a>(), seg_err);
-  }
-  {
     StageTimer t(S_LINES, st);
-    launch_lines(st, g.H.as<g2a>(), NP, g.lines.as<uint32_t>());
+    launch_lines(st, g.H.as<g2a>(), 0, N, NP, g.lines.as<uint32_t>());
   }
+  HIPCHK(hipEventRecord(g.ev_side1, g.side1));
+  HIPCHK(hipEventRecord(g.ev_side2, g.side2));
+  HIPCHK(hipStreamWaitEvent(st, g.ev_side1, 0));
+  HIPCHK(hipStreamWaitEvent(st, g.ev_side2, 0));
   {
     StageTimer t(S_ML_LEAF, st);
-    launch_ml_leaf(st, g.lines.as<uint32_t>(), NP, g.P.as<g1a>(), g.tab.as<uint32_t>(),
-                   (uint32_t)ncouple, g.V0.as<fp12>());
+    launch_ml_leaf(st, g.lines.as<uint32_t>(), NP, g.P.as<g1a>(), T, (uint32_t)ncouple,
+                   g.V0.as<fp12>());
   }
   fp12 *cur = g.V0.as<fp12>(), *other = g.V1.as<fp12>();
   {
     StageTimer t(S_ML_REDUCE, st);
     for (const Level &L : levels) {
-      launch_ml_reduce(st, cur, (uint32_t)L.nin, g.tab.as<uint32_t>() + L.tab_off, (uint32_t)L.nout,
-                       other);
+      launch_ml_reduce(st, cur, (uint32_t)L.nin, T + L.tab_off, (uint32_t)L.nout, other);
       std::swap(cur, other);
     }
   }

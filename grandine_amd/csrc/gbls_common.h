@@ -38,14 +38,18 @@ void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q);
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H);
 
 // k_scalar.hip -- random-scalar products and the per-segment signature sum
-void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, const int32_t *pre,
-                     uint32_t n, g1a *P, int32_t *bad);
+void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1a *P);
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R);
-void launch_seg_g2_sum(hipStream_t st, const g2j *R, const int32_t *bad, const uint32_t *seg_off,
-                       uint32_t nseg, uint32_t n, g1a *P, g2a *H, int32_t *seg_err);
+// chunks: 4 words per level-1 workgroup {segment, half, begin, end}; seg_chunk[nseg+1]
+void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
+                  const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
+                  const g1a *pks, const int32_t *pre, g2j *part, int32_t *part_err, g1a *P, g2a *H,
+                  int32_t *seg_err);
 
 // k_lines.hip -- Miller-loop line functions of every pair
-void launch_lines(hipStream_t st, const g2a *H, uint32_t np, uint32_t *lines);
+// lines of pairs [first, first + count) of np (H indexed by pair)
+void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
+                  uint32_t *lines);
 
 // k_miller.hip -- Miller product tree + Horner
 void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1a *P,

@@ -5,15 +5,17 @@
 
 namespace gbls {
 
-__global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t np, uint32_t *L) {
+__global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t first, uint32_t count,
+                                              uint32_t np, uint32_t *L) {
   uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= np) return;
-  g2a q = H[i];
-  lines_of(L, np, i, q);
+  if (i >= count) return;
+  g2a q = H[first + i];
+  lines_of(L, np, first + i, q);
 }
 
-void launch_lines(hipStream_t st, const g2a *H, uint32_t np, uint32_t *lines) {
-  k_lines<<<nblk(np), WG, 0, st>>>(H, np, lines);
+void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
+                  uint32_t *lines) {
+  if (count) k_lines<<<nblk(count), WG, 0, st>>>(H, first, count, np, lines);
 }
 
 }  // namespace gbls

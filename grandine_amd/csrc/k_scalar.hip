@@ -1,15 +1,16 @@
 // gfx950 kernels: the random linear combination of Signature::multi_verify
 // (bls/src/signature.rs:106-126): P_i = r_i pk_i (G1, one lane per set) and
-// S = sum r_i sig_i (G2, one lane per set + a workgroup tree per segment).
+// S = sum r_i sig_i (G2).  The G2 side splits every 64-bit scalar into 32-bit halves
+// (two lanes per set, half the serial chain): S = S_lo + [2^32] S_hi with
+// S_lo = sum [lo(r_i)] sig_i, S_hi = sum [hi(r_i)] sig_i, summed by a two-level
+// workgroup tree.
 #include "gbls_common.h"
 
 namespace gbls {
 
-// P_i = affine(r_i pk_i); bad_i = pk infinite (blst PAIRING_Aggregate_PK_in_G1 rejects
-// it) or a caller pre-check failed (signature subgroup check, aggregation status).
-__global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t *rands,
-                                                 const int32_t *pre, uint32_t n, g1a *P,
-                                                 int32_t *bad) {
+// P_i = affine(r_i pk_i)
+__global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t *rands, uint32_t n,
+                                                 g1a *P) {
   uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
   g1a pk = pks[i];
@@ -19,22 +20,24 @@ __global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t 
   g1a o;
   jac_to_aff(o, t);
   P[i] = o;
-  bad[i] = (aff_is_inf(pk) || (pre && pre[i] != 0)) ? 1 : 0;
 }
 
-// R_i = r_i sig_i (Jacobian); infinite signatures contribute the identity (blst skips
-// them in the G2 accumulation)
+// R[h * n + i] = [32-bit half h of r_i] sig_i (Jacobian); infinite signatures give the
+// identity (blst skips them in the G2 accumulation)
 __global__ void __launch_bounds__(WG) k_mv_g2mul(const g2a *sigs, const uint64_t *rands, uint32_t n,
                                                  g2j *R) {
-  uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  g2j t;
-  mul_u64(t, sigs[i], rands ? rands[i] : 1);
-  R[i] = t;
+  uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= 2 * n) return;
+  uint32_t i = t < n ? t : t - n;
+  uint64_t r = rands ? rands[i] : 1;
+  uint64_t k = t < n ? (r & 0xffffffffull) : (r >> 32);
+  g2j o;
+  mul_u64(o, sigs[i], k);
+  R[t] = o;
 }
 
 template <class F>
-__device__ void wg_reduce_jac2(jac<F> &v) {
+__device__ void wg_reduce_jac(jac<F> &v) {
   __shared__ jac<F> buf[WGR / 2];
   for (int w = WGR / 2; w > 0; w >>= 1) {
     __syncthreads();
@@ -47,48 +50,77 @@ __device__ void wg_reduce_jac2(jac<F> &v) {
   }
 }
 
-// S_s = sum R_i over segment s -> the segment's extra Miller pair (-g1, S_s) at index
-// n + s of the pair arrays; seg_err[s] = OR bad_i | (segment empty)
-__global__ void __launch_bounds__(WGR) k_seg_g2_sum(const g2j *R, const int32_t *bad,
-                                                    const uint32_t *off, uint32_t nseg, uint32_t n,
-                                                    g1a *P, g2a *H, int32_t *seg_err) {
+// level 1: workgroup c sums R[h*n + b .. h*n + e) (chunk table: {s, h, b, e}) and ORs the
+// bad flags (pk infinite -- blst PAIRING_Aggregate_PK_in_G1 -- or a failed pre-check)
+__global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32_t *chunks, uint32_t n,
+                                                      const g1a *pks, const int32_t *pre, g2j *part,
+                                                      int32_t *part_err) {
   __shared__ int32_t e_sh;
-  uint32_t s = blockIdx.x;
-  if (s >= nseg) return;
+  uint32_t c = blockIdx.x;
+  uint32_t h = chunks[4 * c + 1], b = chunks[4 * c + 2], e = chunks[4 * c + 3];
   if (threadIdx.x == 0) e_sh = 0;
   __syncthreads();
   g2j acc;
   jac_set_inf(acc);
-  int32_t e = 0;
-  for (uint32_t i = off[s] + threadIdx.x; i < off[s + 1]; i += WGR) {
-    g2j r = R[i];
+  int32_t bad = 0;
+  for (uint32_t i = b + threadIdx.x; i < e; i += WGR) {
+    g2j r = R[(size_t)h * n + i];
     jac_add(acc, acc, r);
-    e |= bad[i];
+    if (h == 0) bad |= (aff_is_inf(pks[i]) || (pre && pre[i] != 0)) ? 1 : 0;
   }
-  if (e) atomicOr(&e_sh, 1);
-  wg_reduce_jac2(acc);
+  if (bad) atomicOr(&e_sh, 1);
+  wg_reduce_jac(acc);
   if (threadIdx.x == 0) {
-    g1a ng1;
-    fp_set(ng1.x, k::G1X_M);
-    fp_set(ng1.y, k::G1NEGY_M);
-    g2a q;
-    jac_to_aff(q, acc);
-    P[n + s] = ng1;
-    H[n + s] = q;
-    seg_err[s] = e_sh | (off[s + 1] == off[s] ? 1 : 0);
+    part[c] = acc;
+    part_err[c] = e_sh;
   }
 }
 
-void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, const int32_t *pre,
-                     uint32_t n, g1a *P, int32_t *bad) {
-  k_mv_g1mul<<<nblk(n), WG, 0, st>>>(pks, rands, pre, n, P, bad);
+// level 2: one lane per segment: S = S_lo + [2^32] S_hi over the segment's chunks, then
+// the segment's extra Miller pair (-g1, S) at index n + s; seg_err[s] = OR bad | empty
+__global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32_t *part_err,
+                                                    const uint32_t *chunks, const uint32_t *seg_chunk,
+                                                    const uint32_t *seg_off, uint32_t nseg, uint32_t n,
+                                                    g1a *P, g2a *H, int32_t *seg_err) {
+  uint32_t s = blockIdx.x * WG + threadIdx.x;
+  if (s >= nseg) return;
+  g2j lo, hi;
+  jac_set_inf(lo);
+  jac_set_inf(hi);
+  int32_t err = seg_off[s + 1] == seg_off[s] ? 1 : 0;
+  for (uint32_t c = seg_chunk[s]; c < seg_chunk[s + 1]; c++) {
+    g2j v = part[c];
+    if (chunks[4 * c + 1] == 0)
+      jac_add(lo, lo, v);
+    else
+      jac_add(hi, hi, v);
+    err |= part_err[c];
+  }
+  for (int j = 0; j < 32; j++) jac_dbl(hi, hi);
+  jac_add(lo, lo, hi);
+  g1a ng1;
+  fp_set(ng1.x, k::G1X_M);
+  fp_set(ng1.y, k::G1NEGY_M);
+  g2a q;
+  jac_to_aff(q, lo);
+  P[n + s] = ng1;
+  H[n + s] = q;
+  seg_err[s] = err;
+}
+
+void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1a *P) {
+  k_mv_g1mul<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
 }
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R) {
-  k_mv_g2mul<<<nblk(n), WG, 0, st>>>(sigs, rands, n, R);
+  k_mv_g2mul<<<nblk(2 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
 }
-void launch_seg_g2_sum(hipStream_t st, const g2j *R, const int32_t *bad, const uint32_t *seg_off,
-                       uint32_t nseg, uint32_t n, g1a *P, g2a *H, int32_t *seg_err) {
-  k_seg_g2_sum<<<nseg, WGR, 0, st>>>(R, bad, seg_off, nseg, n, P, H, seg_err);
+void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
+                  const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
+                  const g1a *pks, const int32_t *pre, g2j *part, int32_t *part_err, g1a *P, g2a *H,
+                  int32_t *seg_err) {
+  k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, pre, part, part_err);
+  k_g2sum_final<<<nblk(nseg), WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n, P, H,
+                                           seg_err);
 }
 
 }  // namespace gbls
