@@ -10,9 +10,11 @@ namespace gbls {
 __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const int32_t *err,
                                                       uint32_t nparts, uint32_t nseg,
                                                       int32_t *verdict) {
-  __shared__ uint32_t f[W12_WORDS], F[W12_WORDS], A[W12_WORDS], B[W12_WORDS], T[W12_WORDS],
+  W12_SHARED uint32_t f[W12_WORDS], F[W12_WORDS], A[W12_WORDS], B[W12_WORDS], T[W12_WORDS],
       X[W12_WORDS], ws[W12_WS_WORDS];
   __shared__ int bad;
+  w12_plan pl;
+  w12_begin(pl, ws);
   uint32_t s = blockIdx.x;
   int lane = threadIdx.x;
   const uint32_t *src = reinterpret_cast<const uint32_t *>(part + s);
@@ -24,36 +26,36 @@ __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const in
     for (int i = lane; i < W12_WORDS; i += 64) X[i] = src[i];
     if (lane == 0) bad |= err[(size_t)k2 * nseg + s];
     __syncthreads();
-    w12_mul(f, f, X, ws);
+    w12_mul(pl, f, f, X, ws);
   }
   // easy part: F = (conj(f) f^-1)^(p^2+1)
   w12_inv(X, f);
   w12_conj(A, f);
-  w12_mul(A, A, X, ws);
+  w12_mul(pl, A, A, X, ws);
   w12_frob2(F, A);
-  w12_mul(F, F, A, ws);
+  w12_mul(pl, F, F, A, ws);
   // A = F^(x-1) = F^x conj(F);  A = A^(x-1)
-  w12_cyc_exp_x(A, F, ws);
+  w12_cyc_exp_x(pl, A, F, ws);
   w12_conj(X, F);
-  w12_mul(A, A, X, ws);
-  w12_cyc_exp_x(B, A, ws);
+  w12_mul(pl, A, A, X, ws);
+  w12_cyc_exp_x(pl, B, A, ws);
   w12_conj(X, A);
-  w12_mul(A, B, X, ws);
+  w12_mul(pl, A, B, X, ws);
   // B = A^(x+p) = A^x frob(A)
-  w12_cyc_exp_x(B, A, ws);
+  w12_cyc_exp_x(pl, B, A, ws);
   w12_frob(X, A);
-  w12_mul(B, B, X, ws);
+  w12_mul(pl, B, B, X, ws);
   // T = B^x;  C = T^x frob2(B) conj(B)   (C in A)
-  w12_cyc_exp_x(T, B, ws);
-  w12_cyc_exp_x(A, T, ws);
+  w12_cyc_exp_x(pl, T, B, ws);
+  w12_cyc_exp_x(pl, A, T, ws);
   w12_frob2(X, B);
-  w12_mul(A, A, X, ws);
+  w12_mul(pl, A, A, X, ws);
   w12_conj(X, B);
-  w12_mul(A, A, X, ws);
+  w12_mul(pl, A, A, X, ws);
   // R = C F^3
-  w12_mul(X, F, F, ws);
-  w12_mul(X, X, F, ws);
-  w12_mul(A, A, X, ws);
+  w12_mul(pl, X, F, F, ws);
+  w12_mul(pl, X, X, F, ws);
+  w12_mul(pl, A, A, X, ws);
   if (lane == 0) verdict[s] = (!bad && w12_is_one_image(A)) ? ST_SUCCESS : ST_VERIFY_FAIL;
 }
 

@@ -48,7 +48,9 @@ __device__ __forceinline__ void w12_store(fp12 *dst, const uint32_t *src) {
 // grid (nout, 68): output q of event e = product of Vin[e][red[2q] .. red[2q]+red[2q+1])
 __global__ void __launch_bounds__(64) k_ml_reduce(const fp12 *Vin, uint32_t nin, const uint32_t *red,
                                                   uint32_t nout, fp12 *Vout) {
-  __shared__ uint32_t acc[W12_WORDS], tmp[W12_WORDS], ws[W12_WS_WORDS];
+  W12_SHARED uint32_t acc[W12_WORDS], tmp[W12_WORDS], ws[W12_WS_WORDS];
+  w12_plan pl;
+  w12_begin(pl, ws);
   uint32_t q = blockIdx.x;
   int e = blockIdx.y;
   uint32_t b = red[2 * q], cnt = red[2 * q + 1];
@@ -56,20 +58,22 @@ __global__ void __launch_bounds__(64) k_ml_reduce(const fp12 *Vin, uint32_t nin,
   w12_load(acc, src);
   for (uint32_t j = 1; j < cnt; j++) {
     w12_load(tmp, src + j);
-    w12_mul(acc, acc, tmp, ws);
+    w12_mul(pl, acc, acc, tmp, ws);
   }
   w12_store(Vout + (size_t)e * nout + q, acc);
 }
 
 // grid nseg: V holds one value per (event, segment): V[e * nseg + s]
 __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, fp12 *partial) {
-  __shared__ uint32_t acc[W12_WORDS], tmp[W12_WORDS], ws[W12_WS_WORDS];
+  W12_SHARED uint32_t acc[W12_WORDS], tmp[W12_WORDS], ws[W12_WS_WORDS];
+  w12_plan pl;
+  w12_begin(pl, ws);
   uint32_t s = blockIdx.x;
   w12_load(acc, V + s);
   for (int e = 1; e < ML_EVENTS; e++) {
-    if (ev_is_dbl(e)) w12_mul(acc, acc, acc, ws);
+    if (ev_is_dbl(e)) w12_mul(pl, acc, acc, acc, ws);
     w12_load(tmp, V + (size_t)e * nseg + s);
-    w12_mul(acc, acc, tmp, ws);
+    w12_mul(pl, acc, acc, tmp, ws);
   }
   w12_conj(acc, acc);
   w12_store(partial + s, acc);

@@ -128,10 +128,19 @@ uint32_t h_h2c_stages_size() { return sizeof(H2cStages); }
 // runs lanes 0..63 in order, exactly as the single-wave device workgroup does.
 static void w12_mul_host(uint32_t *c, const uint32_t *a, const uint32_t *b) {
   static uint32_t ws[W12_WS_WORDS];
-  for (int l = 0; l < 64; l++) w12_r_mul(l, a, b, ws);
-  for (int l = 0; l < 64; l++) w12_r_post1(l, ws);
-  for (int l = 0; l < 64; l++) w12_r_post2(l, ws);
-  for (int l = 0; l < 64; l++) w12_r_post3(l, ws, c);
+  static w12_plan pl[64];
+  static bool init = false;
+  if (!init) {
+    for (int l = 0; l < 64; l++) {
+      w12_plan_load(pl[l], l);
+      w12_r_ws_init(l, ws);
+    }
+    init = true;
+  }
+  for (int l = 0; l < 64; l++) w12_r_mul(l, pl[l], a, b, ws);
+  for (int l = 0; l < 64; l++) w12_r_post1(l, pl[l], ws);
+  for (int l = 0; l < 64; l++) w12_r_post2(l, pl[l], ws);
+  for (int l = 0; l < 64; l++) w12_r_post3(l, pl[l], ws, c);
 }
 static void w12_conj_host(uint32_t *c, const uint32_t *a) {
   for (int l = 0; l < 64; l++) w12_r_conj(l, a, c);

@@ -105,6 +105,35 @@ def main():
         for terms in rnd:
             assert all(abs(s) == 1 for _, s in terms)
 
+    # ---- per-lane plan: the same maps as register-resident byte lists.  Positive terms
+    # first, then negative ones, padded to the round's maxima with the zero slot, so that
+    # every lane runs the same instruction stream (no sign selects, no divergence).
+    zero = base2 + 18          # index of the all-zero value slot in ws
+    pre_none = 12              # PRE: "no coefficient" -> zero operand
+    rounds = {}
+    for name, rnd in (("POST1", post1), ("POST2", post2), ("POST3", post3)):
+        npos = max(sum(1 for _, g in t if g > 0) for t in rnd)
+        nneg = max(sum(1 for _, g in t if g < 0) for t in rnd)
+        assert npos + nneg <= 8          # (npos + nneg) p < 2^384 and 2 plan words
+        lanes = []
+        for l in range(64):
+            t = rnd[l] if l < len(rnd) else []
+            pos = [s for s, g in t if g > 0] + [zero] * (npos - sum(1 for _, g in t if g > 0))
+            neg = [s for s, g in t if g < 0] + [zero] * (nneg - sum(1 for _, g in t if g < 0))
+            lanes.append(pos + neg + [zero] * (8 - npos - nneg))
+        rounds[name] = (npos, nneg, lanes)
+
+    def pack(bs):
+        return [sum(b << (8 * i) for i, b in enumerate(bs[k:k + 4])) for k in (0, 4)]
+
+    plan = []
+    for l in range(64):
+        pre = prod[l] + [pre_none] * (8 - len(prod[l])) if l < 54 else [pre_none] * 8
+        words = pack(pre)
+        for name in ("POST1", "POST2", "POST3"):
+            words += pack(rounds[name][2][l])
+        plan.append(words)
+
     out = []
     w = out.append
     w("// GENERATED by tools/gen_wave12.py -- do not edit.")
@@ -135,6 +164,15 @@ def main():
             cells = ["{%d, %d}" % (s, g) for s, g in terms] + ["{-1, 0}"] * (T - len(terms))
             w("  {%s}," % ", ".join(cells))
         w("};")
+    w("// Register plan per lane: words 0-1 PRE bytes, 2-3 POST1, 4-5 POST2, 6-7 POST3;")
+    w("// POST bytes: NPOSn positive sources, then NNEGn negative, then padding.")
+    w("constexpr int ZERO_SLOT = %d, PRE_NONE = %d, NSLOT = %d;" % (zero, pre_none, zero + 1))
+    for i, name in enumerate(("POST1", "POST2", "POST3")):
+        w("constexpr int NPOS%d = %d, NNEG%d = %d;" % (i + 1, rounds[name][0], i + 1, rounds[name][1]))
+    w("GBLS_CONSTANT uint32_t PLAN[64][8] = {")
+    for words in plan:
+        w("  {%s}," % ", ".join("0x%08xu" % x for x in words))
+    w("};")
     w("}}  // namespace gbls::w12")
     print("\n".join(out))
 

@@ -13,8 +13,10 @@ using namespace gbls;
 constexpr int ITERS = 256;
 
 __global__ void __launch_bounds__(64) k_bench(const uint32_t *in, uint64_t *out, uint32_t *sink) {
-  __shared__ uint32_t a[W12_WORDS], b[W12_WORDS], ws[W12_WS_WORDS];
+  W12_SHARED uint32_t a[W12_WORDS], b[W12_WORDS], ws[W12_WS_WORDS];
   int lane = threadIdx.x;
+  w12_plan pl;
+  w12_begin(pl, ws);
   for (int i = lane; i < W12_WORDS; i += 64) {
     a[i] = in[i];
     b[i] = in[W12_WORDS + i];
@@ -23,21 +25,21 @@ __global__ void __launch_bounds__(64) k_bench(const uint32_t *in, uint64_t *out,
   uint64_t t_mul = 0, t_p1 = 0, t_p2 = 0, t_p3 = 0;
   uint64_t r0 = __builtin_amdgcn_s_memrealtime();
   uint64_t t0 = clock64();
-  for (int it = 0; it < ITERS; it++) w12_mul(a, a, b, ws);
+  for (int it = 0; it < ITERS; it++) w12_mul(pl, a, a, b, ws);
   uint64_t t1 = clock64();
   uint64_t r1 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < ITERS; it++) {
     uint64_t s0 = clock64();
-    w12_r_mul(lane, a, b, ws);
+    w12_r_mul(lane, pl, a, b, ws);
     __syncthreads();
     uint64_t s1 = clock64();
-    w12_r_post1(lane, ws);
+    w12_r_post1(lane, pl, ws);
     __syncthreads();
     uint64_t s2 = clock64();
-    w12_r_post2(lane, ws);
+    w12_r_post2(lane, pl, ws);
     __syncthreads();
     uint64_t s3 = clock64();
-    w12_r_post3(lane, ws, a);
+    w12_r_post3(lane, pl, ws, a);
     __syncthreads();
     uint64_t s4 = clock64();
     t_mul += s1 - s0;
