@@ -856,6 +856,48 @@ int ref_multi_verify(const uint8_t *msgs32, const uint8_t *sigs192, const uint8_
   final_exp(&r, &f);
   return fe12_is_one(&r);
 }
+/* Sharded multi_verify: one shard's Miller partial
+   F = prod_i ML(r_i pk_i, H(m_i)) * ML(-g1, sum_i r_i sig_i), no final exponentiation.
+   Returns the shard's error flag (an infinite pk). out576 = the Fp12 partial. */
+int ref_multi_verify_partial(const uint8_t *msgs32, const uint8_t *sigs192, const uint8_t *pks96,
+                             const uint64_t *rands, size_t n, uint8_t *out576) {
+  ensure_init();
+  job_t job;
+  memset(&job, 0, sizeof job);
+  job.msgs = msgs32; job.sigs = sigs192; job.pks = pks96; job.rands = rands;
+  job.b = 0; job.e = n;
+  fe12 f = F12ONE;
+  int bad = 0;
+  if (n) {
+    mv_worker(&job);
+    f = job.f;
+    bad = job.bad;
+    if (!p2_is_inf(&job.S)) {
+      p2a Sa;
+      p2_to_aff(&Sa, &job.S);
+      p1a ng1 = G1;
+      fe_neg(&ng1.y, &ng1.y);
+      fe12 g;
+      miller_loop_n(&g, &ng1, &Sa, 1);
+      fe12_mul(&f, &f, &g);
+    }
+  }
+  memcpy(out576, &f, sizeof f);
+  return bad;
+}
+/* product of nparts shard partials, final exponentiation, verdict: 1 = valid */
+int ref_final_verify_partials(const uint8_t *parts576, const int32_t *errs, size_t nparts) {
+  ensure_init();
+  fe12 f = F12ONE, g;
+  for (size_t k = 0; k < nparts; k++) {
+    if (errs[k]) return 0;
+    memcpy(&g, parts576 + 576 * k, 576);
+    fe12_mul(&f, &f, &g);
+  }
+  fe12 r;
+  final_exp(&r, &f);
+  return fe12_is_one(&r);
+}
 /* Signature::verify (sig_groupcheck = true, infinite pk rejected): 1 = valid */
 int ref_verify(const uint8_t *sig192, const uint8_t *msg, size_t len, const uint8_t *pk96) {
   ensure_init();
