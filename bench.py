@@ -76,6 +76,21 @@ def make_workload(G, L, n, seed):
     return msgs, sigs.raw, pks.raw, rands
 
 
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
+    summary of this same command at the same n (profiles/r01/pmc_bytes.csv, written by
+    tools/prof/pmc_bytes.py; FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_bytes.csv")
+    if n != 4096 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        for row in f.read().splitlines()[1:]:
+            cols = row.split(",")
+            if cols[0].split("::")[-1] == kernel:
+                return float(cols[4])
+    return None
+
+
 def cpu_baseline(n_sample, threads):
     """Time the C oracle (oracle/_build/bls_ref, restatement of blst's multi-verify) on a
     bounded sample of the same workload shape; None if the oracle is not built."""
@@ -205,7 +220,7 @@ def main():
         ach = mads / avg_s / 1e12
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4),
                 "peak": round(peak / 1e12, 3), "unit": "Tmad64/s", "frac": round(ach / (peak / 1e12), 5) if peak else None,
-                "traffic": None, "avg_launch_ms": round(tot_ms / ncalls, 4),
+                "traffic": pmc_traffic(dom, n), "avg_launch_ms": round(tot_ms / ncalls, 4),
                 "stage_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()}}
 
     if rank == 0:
