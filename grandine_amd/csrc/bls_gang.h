@@ -1,0 +1,139 @@
+// Quad gangs: four adjacent lanes (one DPP quad) cooperate on one G2 point.
+//
+// A lane-per-point G2 doubling is a serial chain of 2 Fp2 products and 5 Fp2 squarings
+// (16 Fp products).  Its dependency DAG is only three levels deep, so a quad runs each
+// level's independent Fp2 operations side by side, one per lane, as ONE instruction
+// stream with per-lane operands (v_cndmask selects), and shares the results with DPP
+// quad_perm broadcasts (a VALU move, no LDS):
+//
+//   level 1: X^2, Y^2, (Y+Z)^2, Z^2     -> A, B, 2YZ = (Y+Z)^2 - B - Z^2
+//   level 2: B^2, (X+B)^2, E^2 (E = 3A) -> C, D = 2((X+B)^2 - A - C), F
+//   level 3: E (D - X3)                 (one product, every lane)
+//
+// Critical path 2 + 2 + 3 = 7 Fp products instead of 16.  Every lane of the quad ends
+// holding the same point, so the rest of the code (additions, psi, to-affine) runs
+// unchanged and redundantly.  Used by cofactor clearing, the dominant stage of
+// hash_to_G2 (a13; blst Hash_to_G2 -> clear_cofactor via Budroni-Pintore).
+#pragma once
+#include "bls_curve.h"
+
+namespace gbls {
+
+template <int K>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xf, 0xf, false);
+}
+template <int K>
+__device__ __forceinline__ void fp2_quad_bcast(fp2 &r, const fp2 &a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = quad_bcast<K>(a.c0.l[i]);
+    r.c1.l[i] = quad_bcast<K>(a.c1.l[i]);
+  }
+}
+// r = q==0 ? a : q==1 ? b : q==2 ? c : d, limb-wise (no branches)
+__device__ __forceinline__ void fp2_sel4(fp2 &r, int q, const fp2 &a, const fp2 &b, const fp2 &c,
+                                         const fp2 &d) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint32_t x0 = q == 0 ? a.c0.l[i] : b.c0.l[i];
+    uint32_t y0 = q == 2 ? c.c0.l[i] : d.c0.l[i];
+    r.c0.l[i] = q < 2 ? x0 : y0;
+    uint32_t x1 = q == 0 ? a.c1.l[i] : b.c1.l[i];
+    uint32_t y1 = q == 2 ? c.c1.l[i] : d.c1.l[i];
+    r.c1.l[i] = q < 2 ? x1 : y1;
+  }
+}
+
+// dbl-2009-l (a = 0) across a quad; q = lane & 3.  r may alias p.
+__device__ __forceinline__ void gang_dbl(g2j &r, const g2j &p, int q) {
+  fp2 in, s, A, B, W, Z2, E, t;
+  f_add(t, p.y, p.z);
+  fp2_sel4(in, q, p.x, p.y, t, p.z);
+  fp2_sqr(s, in);
+  fp2_quad_bcast<0>(A, s);
+  fp2_quad_bcast<1>(B, s);
+  fp2_quad_bcast<2>(W, s);
+  fp2_quad_bcast<3>(Z2, s);
+  f_add(t, p.x, B);  // X + B          (p.x dead)
+  f_sub(W, W, B);
+  f_sub(r.z, W, Z2);  // Z3 = (Y+Z)^2 - Y^2 - Z^2 = 2YZ
+  f_dbl(E, A);
+  f_add(E, E, A);  // E = 3A
+  fp2_sel4(in, q, B, t, E, E);
+  fp2_sqr(s, in);
+  fp2 C, U, F;
+  fp2_quad_bcast<0>(C, s);
+  fp2_quad_bcast<1>(U, s);
+  fp2_quad_bcast<2>(F, s);
+  f_sub(U, U, A);
+  f_sub(U, U, C);
+  f_dbl(U, U);        // D
+  f_sub(F, F, U);
+  f_sub(r.x, F, U);   // X3 = F - 2D
+  f_sub(t, U, r.x);
+  f_mul(t, E, t);     // E (D - X3)
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_sub(r.y, t, C);   // Y3 = E (D - X3) - 8C
+}
+
+// [|x|]P with quad-cooperative doublings (additions stay per lane)
+__device__ __forceinline__ void gang_mul_by_xabs(g2j &r, const g2j &p, int q) {
+  g2j acc = p;
+  for (int i = 62; i >= 0; i--) {
+    gang_dbl(acc, acc, q);
+    if ((k::X_ABS >> i) & 1) jac_add(acc, acc, p);
+  }
+  r = acc;
+}
+
+}  // namespace gbls
+
+#ifdef GBLS_GANG_LINES
+namespace gbls {
+
+// Miller-loop doubling step (line_dbl, bls_pairing.h) across a quad.  Serial: 3 Fp2
+// products + 5 squarings; here three levels of one Fp2 product each:
+//   level 1: X Y, Y^2, Z^2, X^2
+//   level 2: A (B - F), G^2, E^2, Y Z      (A = XY/2, E = 3b'Z^2, F = 3E, G = (B+F)/2)
+//   level 3: Z3 = B H                      (H = 2YZ, every lane)
+// Line coefficients L0 = E - B, L2 = 3X^2, L3 = -H, as line_dbl.
+__device__ __forceinline__ void gang_line_dbl(g2h &T, fp2 &L0, fp2 &L2, fp2 &L3, int q) {
+  fp2 a, b, s, A, B, C, X2;
+  fp2_sel4(a, q, T.x, T.y, T.z, T.x);
+  fp2_sel4(b, q, T.y, T.y, T.z, T.x);
+  fp2_mul(s, a, b);
+  fp2_quad_bcast<0>(A, s);
+  fp2_quad_bcast<1>(B, s);
+  fp2_quad_bcast<2>(C, s);
+  fp2_quad_bcast<3>(X2, s);
+  fp2_half(A, A);     // XY/2
+  fp2 E, F, G, t1;
+  fp2_mul_3b(E, C);   // 3b'Z^2
+  fp2_add(F, E, E);
+  fp2_add(F, F, E);   // 3E
+  fp2_sub(L0, E, B);
+  fp2_mul3(L2, X2);
+  fp2_sub(t1, B, F);
+  fp2_add(G, B, F);
+  fp2_half(G, G);
+  fp2_sel4(a, q, A, G, E, T.y);
+  fp2_sel4(b, q, t1, G, E, T.z);
+  fp2_mul(s, a, b);
+  fp2 X3, G2, E2, H;
+  fp2_quad_bcast<0>(X3, s);
+  fp2_quad_bcast<1>(G2, s);
+  fp2_quad_bcast<2>(E2, s);
+  fp2_quad_bcast<3>(H, s);
+  fp2_add(H, H, H);   // 2YZ
+  fp2_neg(L3, H);
+  T.x = X3;           // X3 = A (B - F)
+  fp2_mul3(E2, E2);
+  fp2_sub(T.y, G2, E2);  // Y3 = G^2 - 3E^2
+  fp2_mul(T.z, B, H);    // Z3 = B H
+}
+
+}  // namespace gbls
+#endif
