@@ -1,21 +1,60 @@
 // gfx950 kernel: the 68 Miller-loop line functions (63 doubling + 5 addition steps
-// along |x|) of every pair's G2 point, one lane per pair, stored structure-of-arrays
-// (bls_pairing.h line_word) so that each later load is one coalesced dword per lane.
+// along |x|) of every pair's G2 point, stored structure-of-arrays (bls_pairing.h
+// line_word) so that each later load is one coalesced dword per lane.  One DPP quad per
+// pair: doubling steps run quad-cooperatively (bls_gang.h gang_line_dbl), addition steps
+// redundantly in all four lanes; lane q stores line components c with c % 4 == q.
 #include "gbls_common.h"
+#define GBLS_GANG_LINES
+#include "bls_gang.h"
 
 namespace gbls {
 
+__device__ __forceinline__ void line_put_q(uint32_t *L, uint32_t np, uint32_t pair, int e, int q,
+                                           const fp2 &L0, const fp2 &L2, const fp2 &L3) {
+  const fp *v[6] = {&L0.c0, &L0.c1, &L2.c0, &L2.c1, &L3.c0, &L3.c1};
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    if ((c & 3) != q) continue;
+#pragma unroll
+    for (int i = 0; i < 12; i++) L[line_word(e, c, i, np, pair)] = v[c]->l[i];
+  }
+}
+
+// lines_of (bls_pairing.h) with quad doubling steps
 __global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t first, uint32_t count,
                                               uint32_t np, uint32_t *L) {
-  uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= count) return;
-  g2a q = H[first + i];
-  lines_of(L, np, first + i, q);
+  uint32_t t = blockIdx.x * WG + threadIdx.x;
+  uint32_t i = t >> 2;
+  int q = (int)(t & 3);
+  if (i >= count) return;  // whole quads only
+  uint32_t pair = first + i;
+  g2a Q = H[pair];
+  fp2 L0, L2, L3;
+  if (aff_is_inf(Q)) {
+    fp2_one(L0);
+    fp2_zero(L2);
+    fp2_zero(L3);
+    for (int e = 0; e < ML_EVENTS; e++) line_put_q(L, np, pair, e, q, L0, L2, L3);
+    return;
+  }
+  g2h T;
+  T.x = Q.x;
+  T.y = Q.y;
+  fp2_one(T.z);
+  int e = 0;
+  for (int b = 62; b >= 0; b--) {
+    gang_line_dbl(T, L0, L2, L3, q);
+    line_put_q(L, np, pair, e++, q, L0, L2, L3);
+    if ((k::X_ABS >> b) & 1) {
+      line_add_aff(T, Q, L0, L2, L3);
+      line_put_q(L, np, pair, e++, q, L0, L2, L3);
+    }
+  }
 }
 
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
                   uint32_t *lines) {
-  if (count) k_lines<<<nblk(count), WG, 0, st>>>(H, first, count, np, lines);
+  if (count) k_lines<<<nblk((size_t)count * 4), WG, 0, st>>>(H, first, count, np, lines);
 }
 
 }  // namespace gbls
