@@ -79,12 +79,86 @@ __device__ __forceinline__ void gang_dbl(g2j &r, const g2j &p, int q) {
   f_sub(r.y, t, C);   // Y3 = E (D - X3) - 8C
 }
 
-// [|x|]P with quad-cooperative doublings (additions stay per lane)
+// add-2007-bl (jac_add, bls_curve.h) across a quad, r = a + b, r may alias a.  Serial:
+// 11 Fp2 products + 5 squarings; here five levels of one Fp2 product each:
+//   level 1: Z1^2, Z2^2, Y1 Z2, Y2 Z1
+//   level 2: U1 = X1 Z2Z2, U2 = X2 Z1Z1, S1 = Y1Z2 Z2Z2, S2 = Y2Z1 Z1Z1   (H, r)
+//   level 3: I = (2H)^2, r^2, (Z1 + Z2)^2
+//   level 4: J = H I, V = U1 I, Z3 = 2 Z1 Z2 H
+//   level 5: r (V - X3), S1 J
+// The degenerate branches depend only on values every lane of the quad shares.
+__device__ __forceinline__ void gang_add(g2j &r, const g2j &a, const g2j &b, int q) {
+  if (jac_is_inf(b)) {
+    r = a;
+    return;
+  }
+  if (jac_is_inf(a)) {
+    r = b;
+    return;
+  }
+  fp2 x, y, s, Z1Z1, Z2Z2, U1, U2, S1, S2;
+  fp2_sel4(x, q, a.z, b.z, a.y, b.y);
+  fp2_sel4(y, q, a.z, b.z, b.z, a.z);
+  fp2_mul(s, x, y);
+  fp2_quad_bcast<0>(Z1Z1, s);
+  fp2_quad_bcast<1>(Z2Z2, s);
+  fp2_quad_bcast<2>(S1, s);
+  fp2_quad_bcast<3>(S2, s);
+  fp2_sel4(x, q, a.x, b.x, S1, S2);
+  fp2_sel4(y, q, Z2Z2, Z1Z1, Z2Z2, Z1Z1);
+  fp2_mul(s, x, y);
+  fp2_quad_bcast<0>(U1, s);
+  fp2_quad_bcast<1>(U2, s);
+  fp2_quad_bcast<2>(S1, s);
+  fp2_quad_bcast<3>(S2, s);
+  fp2 H, R, t;
+  fp2_sub(H, U2, U1);
+  fp2_sub(R, S2, S1);
+  fp2_add(R, R, R);  // r = 2 (S2 - S1)
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(R)) {
+      gang_dbl(r, b, q);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  fp2 H2, ZZ, I, R2, Zs;
+  fp2_add(H2, H, H);
+  fp2_add(ZZ, a.z, b.z);
+  fp2_sel4(x, q, H2, R, ZZ, ZZ);
+  fp2_mul(s, x, x);
+  fp2_quad_bcast<0>(I, s);
+  fp2_quad_bcast<1>(R2, s);
+  fp2_quad_bcast<2>(Zs, s);
+  fp2_sub(Zs, Zs, Z1Z1);
+  fp2_sub(Zs, Zs, Z2Z2);  // 2 Z1 Z2
+  fp2 J, V;
+  fp2_sel4(x, q, H, U1, Zs, Zs);
+  fp2_sel4(y, q, I, I, H, H);
+  fp2_mul(s, x, y);
+  fp2_quad_bcast<0>(J, s);
+  fp2_quad_bcast<1>(V, s);
+  fp2_quad_bcast<2>(r.z, s);  // Z3 = 2 Z1 Z2 H   (a.z, b.z dead)
+  fp2_sub(t, R2, J);
+  fp2_sub(t, t, V);
+  fp2_sub(r.x, t, V);         // X3 = r^2 - J - 2V
+  fp2_sub(t, V, r.x);
+  fp2_sel4(x, q, R, S1, R, S1);
+  fp2_sel4(y, q, t, J, t, J);
+  fp2_mul(s, x, y);
+  fp2_quad_bcast<0>(t, s);
+  fp2_quad_bcast<1>(S1, s);
+  fp2_add(S1, S1, S1);
+  fp2_sub(r.y, t, S1);        // Y3 = r (V - X3) - 2 S1 J
+}
+
+// [|x|]P with quad-cooperative doublings and additions
 __device__ __forceinline__ void gang_mul_by_xabs(g2j &r, const g2j &p, int q) {
   g2j acc = p;
   for (int i = 62; i >= 0; i--) {
     gang_dbl(acc, acc, q);
-    if ((k::X_ABS >> i) & 1) jac_add(acc, acc, p);
+    if ((k::X_ABS >> i) & 1) gang_add(acc, acc, p, q);
   }
   r = acc;
 }

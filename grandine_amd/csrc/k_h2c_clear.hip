@@ -1,7 +1,7 @@
 // gfx950 kernels: hash_to_G2 (a13, RFC 9380 BLS12381G2_XMD:SHA-256_SSWU_RO_ with the
 // Ethereum POP DST, bls/src/consts.rs:1) stage 3 (Q0 + Q1, cofactor clearing, affine).
-// One DPP quad (4 lanes) per message: the 126 doublings of the two [|x|] chains run
-// quad-cooperatively (bls_gang.h); additions, psi and the affine conversion run
+// One DPP quad (4 lanes) per message: the doublings and additions run quad-cooperatively
+// (bls_gang.h); psi and the affine conversion run
 // redundantly in all four lanes and lane 0 stores.  Output: affine points (Miller-loop
 // input).
 #include "gbls_common.h"
@@ -9,25 +9,25 @@
 
 namespace gbls {
 
-// Same sequence as clear_cofactor_g2 (bls_hash.h), with quad doublings.
+// Same sequence as clear_cofactor_g2 (bls_hash.h), with quad doublings and additions.
 __device__ __forceinline__ void gang_clear_cofactor_g2(g2j &r, const g2j &p, int q) {
   g2j t1, t2, t3;
   gang_mul_by_xabs(t1, p, q);
   jac_neg(t1, t1);        // t1 = [x]P
   g2_psi(t2, p);
-  jac_add(t2, t2, t1);    // t1 + psi(P)
+  gang_add(t2, t2, t1, q);    // t1 + psi(P)
   gang_mul_by_xabs(t3, t2, q);
   jac_neg(t3, t3);        // t3 = [x](t1 + psi(P))
   jac_neg(t1, t1);
-  jac_add(t3, t3, t1);    // - t1
+  gang_add(t3, t3, t1, q);    // - t1
   gang_dbl(t1, p, q);
   g2_psi2(t1, t1);
-  jac_add(t3, t3, t1);    // + psi^2(2P)
+  gang_add(t3, t3, t1, q);    // + psi^2(2P)
   g2_psi(t1, p);
   jac_neg(t1, t1);
-  jac_add(t3, t3, t1);    // - psi(P)
+  gang_add(t3, t3, t1, q);    // - psi(P)
   jac_neg(t1, p);
-  jac_add(r, t3, t1);     // - P
+  gang_add(r, t3, t1, q);     // - P
 }
 
 // stage 3: Q0 + Q1, clear the cofactor (Budroni-Pintore), affine.  4 lanes per message;
@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(WG) k_h2c_clear(const g2j *Q, uint32_t n, g2a 
   int q = (int)(t & 3);
   if (i >= n) return;
   g2j a = Q[2 * i], b = Q[2 * i + 1], h;
-  jac_add(a, a, b);
+  gang_add(a, a, b, q);
   gang_clear_cofactor_g2(h, a, q);
   g2a o;
   jac_to_aff(o, h);

@@ -5,6 +5,7 @@
 // S_lo = sum [lo(r_i)] sig_i, S_hi = sum [hi(r_i)] sig_i, summed by a two-level
 // workgroup tree.
 #include "gbls_common.h"
+#include "bls_gang.h"
 
 namespace gbls {
 
@@ -24,16 +25,32 @@ __global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t 
 
 // R[h * n + i] = [32-bit half h of r_i] sig_i (Jacobian); infinite signatures give the
 // identity (blst skips them in the G2 accumulation)
+// r.sigma, split into two 32-bit halves, each half on one DPP quad (quad doublings,
+// bls_gang.h, and quad additions with Z2 = 1); lane 0 of the quad stores.
 __global__ void __launch_bounds__(WG) k_mv_g2mul(const g2a *sigs, const uint64_t *rands, uint32_t n,
                                                  g2j *R) {
-  uint32_t t = blockIdx.x * WG + threadIdx.x;
-  if (t >= 2 * n) return;
+  uint32_t u = blockIdx.x * WG + threadIdx.x;
+  uint32_t t = u >> 2;
+  int q = (int)(u & 3);
+  if (t >= 2 * n) return;  // whole quads only
   uint32_t i = t < n ? t : t - n;
   uint64_t r = rands ? rands[i] : 1;
   uint64_t k = t < n ? (r & 0xffffffffull) : (r >> 32);
-  g2j o;
-  mul_u64(o, sigs[i], k);
-  R[t] = o;
+  g2a base = sigs[i];
+  g2j acc;
+  jac_set_inf(acc);
+  if (k != 0 && !aff_is_inf(base)) {
+    int top = 63;
+    while (!((k >> top) & 1)) top--;
+    g2j bj;
+    jac_from_aff(bj, base);
+    acc = bj;
+    for (int b = top - 1; b >= 0; b--) {
+      gang_dbl(acc, acc, q);
+      if ((k >> b) & 1) gang_add(acc, acc, bj, q);
+    }
+  }
+  if (q == 0) R[t] = acc;
 }
 
 template <class F>
@@ -78,33 +95,58 @@ __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32
 
 // level 2: one lane per segment: S = S_lo + [2^32] S_hi over the segment's chunks, then
 // the segment's extra Miller pair (-g1, S) at index n + s; seg_err[s] = OR bad | empty
+// One wave per segment: 16 DPP quads each fold a strided subset of the segment's chunk
+// partials (quad additions), then a 4-level LDS tree joins the 16 quads; quad 0 applies
+// the 2^32 shift of the high halves and converts to affine.
 __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32_t *part_err,
                                                     const uint32_t *chunks, const uint32_t *seg_chunk,
                                                     const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                                                     g1a *P, g2a *H, int32_t *seg_err) {
-  uint32_t s = blockIdx.x * WG + threadIdx.x;
-  if (s >= nseg) return;
+  constexpr int NQ = WG / 4;
+  __shared__ g2j sh_lo[NQ], sh_hi[NQ];
+  __shared__ int32_t sh_err[NQ];
+  uint32_t s = blockIdx.x;  // grid = nseg exactly
+  int w = (int)(threadIdx.x >> 2), q = (int)(threadIdx.x & 3);
   g2j lo, hi;
   jac_set_inf(lo);
   jac_set_inf(hi);
-  int32_t err = seg_off[s + 1] == seg_off[s] ? 1 : 0;
-  for (uint32_t c = seg_chunk[s]; c < seg_chunk[s + 1]; c++) {
+  int32_t err = 0;
+  for (uint32_t c = seg_chunk[s] + w; c < seg_chunk[s + 1]; c += NQ) {
     g2j v = part[c];
     if (chunks[4 * c + 1] == 0)
-      jac_add(lo, lo, v);
+      gang_add(lo, lo, v, q);
     else
-      jac_add(hi, hi, v);
+      gang_add(hi, hi, v, q);
     err |= part_err[c];
   }
-  for (int j = 0; j < 32; j++) jac_dbl(hi, hi);
-  jac_add(lo, lo, hi);
+  for (int width = NQ / 2; width > 0; width >>= 1) {
+    __syncthreads();
+    if (q == 0 && w >= width && w < 2 * width) {
+      sh_lo[w - width] = lo;
+      sh_hi[w - width] = hi;
+      sh_err[w - width] = err;
+    }
+    __syncthreads();
+    if (w < width) {
+      g2j o = sh_lo[w];
+      gang_add(lo, lo, o, q);
+      o = sh_hi[w];
+      gang_add(hi, hi, o, q);
+      err |= sh_err[w];
+    }
+  }
+  if (w != 0) return;
+  if (seg_off[s + 1] == seg_off[s]) err = 1;
+  for (int j = 0; j < 32; j++) gang_dbl(hi, hi, q);
+  gang_add(lo, lo, hi, q);
   g1a ng1;
   fp_set(ng1.x, k::G1X_M);
   fp_set(ng1.y, k::G1NEGY_M);
-  g2a q;
-  jac_to_aff(q, lo);
+  g2a a;
+  jac_to_aff(a, lo);
+  if (q != 0) return;
   P[n + s] = ng1;
-  H[n + s] = q;
+  H[n + s] = a;
   seg_err[s] = err;
 }
 
@@ -112,14 +154,14 @@ void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint
   k_mv_g1mul<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
 }
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R) {
-  k_mv_g2mul<<<nblk(2 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
+  k_mv_g2mul<<<nblk(8 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
 }
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                   const g1a *pks, const int32_t *pre, g2j *part, int32_t *part_err, g1a *P, g2a *H,
                   int32_t *seg_err) {
   k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, pre, part, part_err);
-  k_g2sum_final<<<nblk(nseg), WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n, P, H,
+  k_g2sum_final<<<nseg, WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n, P, H,
                                            seg_err);
 }
 
