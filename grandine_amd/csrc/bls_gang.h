@@ -8,9 +8,10 @@
 //
 //   level 1: X^2, Y^2, (Y+Z)^2, Z^2     -> A, B, 2YZ = (Y+Z)^2 - B - Z^2
 //   level 2: B^2, (X+B)^2, E^2 (E = 3A) -> C, D = 2((X+B)^2 - A - C), F
-//   level 3: E (D - X3)                 (one product, every lane)
+//   level 3: E (D - X3)                 (Karatsuba terms on lanes 0-2)
 //
-// Critical path 2 + 2 + 3 = 7 Fp products instead of 16.  Every lane of the quad ends
+// Critical path 2 + 2 + 1 = 5 Fp products instead of 16 (the level-3 product's three
+// Karatsuba terms go to three lanes, gang_fp2_mul).  Every lane of the quad ends
 // holding the same point, so the rest of the code (additions, psi, to-affine) runs
 // unchanged and redundantly.  Used by cofactor clearing, the dominant stage of
 // hash_to_G2 (a13; blst Hash_to_G2 -> clear_cofactor via Budroni-Pintore).
@@ -30,6 +31,32 @@ __device__ __forceinline__ void fp2_quad_bcast(fp2 &r, const fp2 &a) {
     r.c0.l[i] = quad_bcast<K>(a.c0.l[i]);
     r.c1.l[i] = quad_bcast<K>(a.c1.l[i]);
   }
+}
+template <int K>
+__device__ __forceinline__ void fp_quad_bcast(fp &r, const fp &a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = quad_bcast<K>(a.l[i]);
+}
+// Fp2 product with its three Karatsuba Fp products spread over lanes 0-2 of the quad
+// (lane 3 duplicates lane 2): one Fp product of latency instead of three.  r = a b in
+// every lane; r may alias a or b.
+__device__ __forceinline__ void gang_fp2_mul(fp2 &r, const fp2 &a, const fp2 &b, int q) {
+  fp x, y, p, t0, t1, t2;
+  fp sa, sb;
+  fp_add(sa, a.c0, a.c1);
+  fp_add(sb, b.c0, b.c1);
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    x.l[i] = q == 0 ? a.c0.l[i] : (q == 1 ? a.c1.l[i] : sa.l[i]);
+    y.l[i] = q == 0 ? b.c0.l[i] : (q == 1 ? b.c1.l[i] : sb.l[i]);
+  }
+  fp_mul(p, x, y);
+  fp_quad_bcast<0>(t0, p);
+  fp_quad_bcast<1>(t1, p);
+  fp_quad_bcast<2>(t2, p);
+  fp_sub(r.c0, t0, t1);
+  fp_add(t0, t0, t1);
+  fp_sub(r.c1, t2, t0);
 }
 // r = q==0 ? a : q==1 ? b : q==2 ? c : d, limb-wise (no branches)
 __device__ __forceinline__ void fp2_sel4(fp2 &r, int q, const fp2 &a, const fp2 &b, const fp2 &c,
@@ -72,7 +99,7 @@ __device__ __forceinline__ void gang_dbl(g2j &r, const g2j &p, int q) {
   f_sub(F, F, U);
   f_sub(r.x, F, U);   // X3 = F - 2D
   f_sub(t, U, r.x);
-  f_mul(t, E, t);     // E (D - X3)
+  gang_fp2_mul(t, E, t, q);  // E (D - X3)
   f_dbl(C, C);
   f_dbl(C, C);
   f_dbl(C, C);
@@ -172,7 +199,7 @@ namespace gbls {
 // products + 5 squarings; here three levels of one Fp2 product each:
 //   level 1: X Y, Y^2, Z^2, X^2
 //   level 2: A (B - F), G^2, E^2, Y Z      (A = XY/2, E = 3b'Z^2, F = 3E, G = (B+F)/2)
-//   level 3: Z3 = B H                      (H = 2YZ, every lane)
+//   level 3: Z3 = B H                      (H = 2YZ, Karatsuba terms on lanes 0-2)
 // Line coefficients L0 = E - B, L2 = 3X^2, L3 = -H, as line_dbl.
 __device__ __forceinline__ void gang_line_dbl(g2h &T, fp2 &L0, fp2 &L2, fp2 &L3, int q) {
   fp2 a, b, s, A, B, C, X2;
@@ -206,7 +233,7 @@ __device__ __forceinline__ void gang_line_dbl(g2h &T, fp2 &L0, fp2 &L2, fp2 &L3,
   T.x = X3;           // X3 = A (B - F)
   fp2_mul3(E2, E2);
   fp2_sub(T.y, G2, E2);  // Y3 = G^2 - 3E^2
-  fp2_mul(T.z, B, H);    // Z3 = B H
+  gang_fp2_mul(T.z, B, H, q);  // Z3 = B H
 }
 
 }  // namespace gbls
