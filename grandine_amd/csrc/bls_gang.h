@@ -236,5 +236,56 @@ __device__ __forceinline__ void gang_line_dbl(g2h &T, fp2 &L0, fp2 &L2, fp2 &L3,
   gang_fp2_mul(T.z, B, H, q);  // Z3 = B H
 }
 
+// Miller-loop addition step (line_add_aff, bls_pairing.h) across a quad, four levels of
+// one Fp2 product per lane (serial: 11 products + 2 squarings):
+//   level 1: y2 Z1, x2 Z1                       -> theta, lambda
+//   level 2: theta x2, lambda y2, theta^2, lambda^2
+//   level 3: lambda^3, lambda^2 X1, theta^2 Z1   -> A
+//   level 4: lambda A, theta (R - A), lambda^3 Y1, lambda^3 Z1
+__device__ __forceinline__ void gang_line_add_aff(g2h &T, const g2a &Q, fp2 &L0, fp2 &L2, fp2 &L3,
+                                                  int q) {
+  fp2 a, b, s, yZ, xZ, th, la;
+  fp2_sel4(a, q, Q.y, Q.x, Q.y, Q.x);
+  fp2_mul(s, a, T.z);
+  fp2_quad_bcast<0>(yZ, s);
+  fp2_quad_bcast<1>(xZ, s);
+  fp2_sub(th, T.y, yZ);
+  fp2_sub(la, T.x, xZ);
+  fp2_sel4(a, q, th, la, th, la);
+  fp2_sel4(b, q, Q.x, Q.y, th, la);
+  fp2_mul(s, a, b);
+  fp2 P0, P1, uu, vv;
+  fp2_quad_bcast<0>(P0, s);
+  fp2_quad_bcast<1>(P1, s);
+  fp2_quad_bcast<2>(uu, s);
+  fp2_quad_bcast<3>(vv, s);
+  fp2_sub(L0, P0, P1);  // theta x2 - lambda y2
+  fp2_neg(L2, th);
+  L3 = la;
+  fp2_sel4(a, q, vv, vv, uu, uu);
+  fp2_sel4(b, q, la, T.x, T.z, T.z);
+  fp2_mul(s, a, b);
+  fp2 vvv, R, A, t;
+  fp2_quad_bcast<0>(vvv, s);
+  fp2_quad_bcast<1>(R, s);
+  fp2_quad_bcast<2>(A, s);
+  fp2_neg(vvv, vvv);    // v^3 = -lambda^3
+  fp2_sub(A, A, vvv);
+  fp2_sub(A, A, R);
+  fp2_sub(A, A, R);
+  fp2_sub(t, R, A);
+  fp2_sel4(a, q, la, th, vvv, vvv);
+  fp2_sel4(b, q, A, t, T.y, T.z);
+  fp2_mul(s, a, b);
+  fp2 X3, U, R2;
+  fp2_quad_bcast<0>(X3, s);
+  fp2_quad_bcast<1>(U, s);
+  fp2_quad_bcast<2>(R2, s);
+  fp2_quad_bcast<3>(T.z, s);  // Z3 = v^3 Z1
+  fp2_neg(T.x, X3);           // X3 = v A
+  fp2_neg(U, U);              // u (R - A)
+  fp2_sub(T.y, U, R2);
+}
+
 }  // namespace gbls
 #endif

@@ -1,8 +1,8 @@
 // gfx950 kernel: the 68 Miller-loop line functions (63 doubling + 5 addition steps
 // along |x|) of every pair's G2 point, stored structure-of-arrays (bls_pairing.h
 // line_word) so that each later load is one coalesced dword per lane.  One DPP quad per
-// pair: doubling steps run quad-cooperatively (bls_gang.h gang_line_dbl), addition steps
-// redundantly in all four lanes; lane q stores line components c with c % 4 == q.
+// pair: doubling and addition steps run quad-cooperatively (bls_gang.h gang_line_dbl,
+// gang_line_add_aff); lane q stores line components c with c % 4 == q.
 #include "gbls_common.h"
 #define GBLS_GANG_LINES
 #include "bls_gang.h"
@@ -20,7 +20,7 @@ __device__ __forceinline__ void line_put_q(uint32_t *L, uint32_t np, uint32_t pa
   }
 }
 
-// lines_of (bls_pairing.h) with quad doubling steps
+// lines_of (bls_pairing.h) with quad doubling and addition steps
 __global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t first, uint32_t count,
                                               uint32_t np, uint32_t *L) {
   uint32_t t = blockIdx.x * WG + threadIdx.x;
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t first, uint
     gang_line_dbl(T, L0, L2, L3, q);
     line_put_q(L, np, pair, e++, q, L0, L2, L3);
     if ((k::X_ABS >> b) & 1) {
-      line_add_aff(T, Q, L0, L2, L3);
+      gang_line_add_aff(T, Q, L0, L2, L3, q);
       line_put_q(L, np, pair, e++, q, L0, L2, L3);
     }
   }
