@@ -1,27 +1,36 @@
 #!/usr/bin/env python3
 """Headline benchmark: verified BLS signature sets/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], SURVEY.md 8(d) "C2"): per rank, a synthetic batch of
-4096 single-pubkey signature sets -- interop-style secret keys, distinct 32-byte
-signing roots, sig_i = sk_i * H(m_i), nonzero 64-bit random scalars r_i -- verified by
-ONE random-linear-combination batch check, exactly Signature::multi_verify
-(reference bls/src/signature.rs:95-129, reached from MultiVerifier::finish,
+Default workload (BASELINE.json configs[1], SURVEY.md 8(d) "C2"): per rank, a synthetic
+batch of 4096 single-pubkey signature sets -- seeded secret keys, distinct 32-byte signing
+roots, sig_i = sk_i * H(m_i), nonzero 64-bit random scalars r_i -- verified by ONE
+random-linear-combination batch check, exactly Signature::multi_verify (reference
+bls/src/signature.rs:95-129, reached from MultiVerifier::finish,
 helper_functions/src/verifier.rs:301-323).  A "step" = one multi_verify of the batch,
-inputs already resident in HBM (decompressed points, as blst takes them).
+inputs already resident in HBM (decompressed points, as blst takes them); hash_to_G2 of
+every message, both scalar sides, the Miller product and the final exponentiation all
+run inside the timed region.
 
-N > 1 (torch.distributed.run, one rank per GPU, backend nccl = RCCL): every rank
-verifies its own 4096 sets; the per-rank Miller partial (one Fp12, 576 B) and error
-flag are all-gathered over xGMI, and every rank runs ONE final exponentiation over the
-product.  Weak scaling: value = N * 4096 * steps / max-rank time.
+Other legs (--config): C3 sync-committee fast_aggregate_verify (10,000 messages x 512
+registry keys; unit = messages), C4 an epoch of attestations (2,048 committees over a
+2^20-key registry: key aggregation + multi_verify; unit = sets), C5 Holesky-scale
+(2^20 sets over the GPUs, keys drawn from a 1.7M-key registry), C1 a mainnet-shaped
+block (~131 sets) through the host-pointer ABI: latency, plus 64-set gossip batches.
+
+N > 1 (torch.distributed.run, one rank per GPU, backend nccl = RCCL): every rank verifies
+its own sets; the per-rank Miller partial (one Fp12, 576 B) and error flag are
+all-gathered over xGMI, and every rank runs ONE final exponentiation over the product
+(SURVEY.md 8(e)).  C2/C4 are weak scaling (a fixed batch per GPU), C5 strong (2^20 sets
+in total), C3 needs no exchange (per-message verdicts).
 
 Extra JSON fields: "roofline" (dominant kernel's integer-multiply throughput vs the
-measured v_mad_u64_u32 peak, HIP events on the launch stream) and "cpu_baseline" (the
-C oracle restating blst's multi-verify algorithm, timed on this host's cores).
+measured v_mad_u64_u32 peak, HIP events on the launch stream, W frozen in BASELINE.md 4)
+and "cpu_baseline" (the C oracle, a TEXTBOOK restatement of blst's multi-verify, timed on
+this host's cores).
 """
 
 import argparse
 import ctypes
-import hashlib
 import json
 import os
 import subprocess
@@ -31,11 +40,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-
 # Algorithmic work per unit, in Fp products (12-limb Montgomery, 288 v_mad_u64_u32
-# each), counted from the formulas each kernel executes (DESIGN.md "Roofline").
-# Frozen here; a faster algorithm raises the achieved fraction, never lowers W.
+# each), counted from the formulas each kernel executes (BASELINE.md section 4,
+# tools/count_work.cpp).  Frozen: a faster algorithm raises the achieved fraction,
+# never lowers W.
 MAD_PER_FPMUL = 288
 W_FPMUL = {
     "k_h2c_field": 0,        # SHA-256 only
@@ -50,50 +58,40 @@ W_FPMUL = {
     "k_ml_reduce": 54 * 68 // 2,  # per pair: 68 events x ~1/2 dense product
     "k_ml_horner": 0,
     "k_final_verdict": 0,
+    "k_g1_aggregate_idx": 11,  # per aggregated key: one mixed G1 addition
 }
 
 
-def interop_sk(i: int) -> bytes:
-    """interop/src/lib.rs:65-76 secret key derivation (big-endian 32 bytes)."""
-    h = hashlib.sha256(i.to_bytes(8, "little") + bytes(24)).digest()
-    return (int.from_bytes(h, "little") % R_ORDER).to_bytes(32, "big")
-
-
-def make_workload(G, L, n, seed):
-    sks = b"".join(interop_sk(seed * 1_000_000 + i) for i in range(n))
-    msgs = b"".join(hashlib.sha256(b"c2/%d/%d" % (seed, i)).digest() for i in range(n))
-    pks = ctypes.create_string_buffer(96 * n)
-    sigs = ctypes.create_string_buffer(192 * n)
-    G.check(L.gbls_sk_to_pk(sks, n, pks), "gbls_sk_to_pk")
-    G.check(L.gbls_sign(sks, msgs, G.u32_array(range(0, 32 * n + 1, 32)), n, sigs), "gbls_sign")
-    x = (seed * 0x9E3779B97F4A7C15 + 12345) & ((1 << 64) - 1)
-    rands = []
-    for _ in range(n):  # xorshift64*: deterministic nonzero scalars
-        x ^= (x >> 12)
-        x ^= (x << 25) & ((1 << 64) - 1)
-        x ^= (x >> 27)
-        rands.append(((x * 0x2545F4914F6CDD1D) & ((1 << 64) - 1)) or 1)
-    return msgs, sigs.raw, pks.raw, rands
+def cpu_threads():
+    """Host cores this process may use: the affinity mask, capped by OMP_NUM_THREADS
+    (the GPU box sets it to this job's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, n)
 
 
 def pmc_traffic(kernel, n):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
-    summary of this same command at the same n (profiles/r01/pmc_bytes.csv, written by
-    tools/prof/pmc_bytes.py; FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_bytes.csv")
-    if n != 4096 or not os.path.exists(path):
-        return None
-    with open(path) as f:
-        for row in f.read().splitlines()[1:]:
-            cols = row.split(",")
-            if cols[0].split("::")[-1] == kernel:
-                return float(cols[4])
+    summary of the default command (profiles/<round>/pmc_bytes.csv, tools/prof/pmc_bytes.py;
+    FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_bytes.csv")
+        if n != 4096 or not os.path.exists(path):
+            continue
+        with open(path) as f:
+            for row in f.read().splitlines()[1:]:
+                cols = row.split(",")
+                if cols[0].split("::")[-1] == kernel:
+                    return float(cols[4])
     return None
 
 
 def cpu_baseline(n_sample, threads):
-    """Time the C oracle (oracle/_build/bls_ref, restatement of blst's multi-verify) on a
-    bounded sample of the same workload shape; None if the oracle is not built."""
+    """Time the C oracle (oracle/_build/bls_ref_bench) on a bounded sample of the C2
+    workload shape; None if the oracle is not built."""
     exe = os.path.join(ROOT, "oracle", "_build", "bls_ref_bench")
     if not os.path.exists(exe):
         return None
@@ -104,8 +102,26 @@ def cpu_baseline(n_sample, threads):
     except Exception as e:  # noqa: BLE001 -- report, never fake a number
         return {"value": None, "unit": "sets/s", "cores": threads, "kind": "port", "error": str(e)[:200]}
     return {"value": rec["sets_per_s"], "unit": "sets/s", "cores": threads, "kind": "port",
-            "sample": "%d-set multi_verify batch (C restatement of blst's algorithm, %d threads)"
-                      % (n_sample, threads), "verdict_ok": rec.get("ok")}
+            "sample": "%d-set multi_verify batch, %d threads: oracle/bls_ref.c, a TEXTBOOK C restatement of "
+                      "blst's multi-verify algorithm (schoolbook Fp2/Fp6, Fermat inversion, plain 1269-bit "
+                      "hard part; no w5 windows / Karatsuba / cyclotomic squaring), so it understates "
+                      "rayon+blst" % (n_sample, threads),
+            "verdict_ok": rec.get("ok")}
+
+
+def to_i64(vals):
+    return [v - (1 << 64) if v >= 1 << 63 else v for v in vals]
+
+
+class Leg:
+    """One benchmark config: device-resident inputs + a step() that enqueues one pass."""
+    metric = "verified BLS signature sets/sec (whole node)"
+    unit = "sets/s"
+    scaling = "weak"
+    units = 0
+
+    def stage_units(self, stage):
+        return self.units
 
 
 def main():
@@ -113,12 +129,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--sets", type=int, default=4096)
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "C5"])
+    ap.add_argument("--sets", type=int, default=0, help="override the per-config batch size")
     ap.add_argument("--cpu-sample", type=int, default=2048)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's host CPU share")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -133,51 +151,150 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from grandine_amd import _lib as G
+    from grandine_amd import factory as F
 
-    L = G.load_library()
-    if L.gbls_init(1 << dev.index, 0) != G.SUCCESS:
-        raise G.EngineUnavailable("gbls_init failed: no gfx950 device")
-    n = args.sets
-    msgs, sigs, pks, rands = make_workload(G, L, n, seed=rank + 1)
+    L = G.lib(1 << dev.index, 0)
 
-    def dev_bytes(b):
-        t = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
-        return t
+    def dbytes(b):
+        return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
 
-    d_msgs, d_sigs, d_pks = dev_bytes(msgs), dev_bytes(sigs), dev_bytes(pks)
-    d_rands = torch.tensor([r - (1 << 64) if r >= (1 << 63) else r for r in rands], dtype=torch.int64,
-                           device=dev)
-    d_verdict = torch.full((1,), -1, dtype=torch.int32, device=dev)
-    d_part = torch.zeros(576, dtype=torch.uint8, device=dev)
-    d_err = torch.zeros(1, dtype=torch.int32, device=dev)
-    d_parts = torch.zeros(world * 576, dtype=torch.uint8, device=dev)
-    d_errs = torch.zeros(world, dtype=torch.int32, device=dev)
-    seg = G.u32_array([0, n])
+    def dnp(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
 
     def ptr(t):
         return ctypes.c_void_p(t.data_ptr())
 
-    def step():
-        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        if world == 1:
-            rc = L.gbls_multi_verify_segments_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n, seg,
-                                                     1, ptr(d_verdict), st)
-            G.check(rc, "multi_verify_segments_device")
+    def cur_stream():
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    leg = Leg()
+    cfg = args.config
+    # ------------------------------------------------------------------ batch-verify legs
+    if cfg in ("C2", "C4", "C5"):
+        if cfg == "C2":
+            n = args.sets or 4096
+            msgs, sigs, pks, rands = F.c2_batch(n, seed=rank + 1)
+            d_pks = dbytes(pks)
+            idx = off = None
+            leg.workload = "C2: %d single-pubkey sets per GPU, random-scalar multi_verify" % n
+        elif cfg == "C4":
+            ncom = args.sets or 2048
+            nreg = 1 << 20
+            nact = nreg - 576  # committee sizes 511/512 (a shuffle remainder)
+            sks, comp = F.registry(nreg, seed=b"c4-registry")
+            assert not F.load_registry(comp).any()
+            idx, off = F.committees(nact, ncom, seed=rank + 4)
+            msgs = F.messages(ncom, b"c4/%d" % rank)
+            sigs, _ = F.committee_signatures(sks, idx, off, msgs)
+            rands = F.rands(ncom, rank + 4)
+            n = ncom
+            leg.pks_per_step = int(off[-1])
+            leg.workload = ("C4: one epoch of attestations per GPU -- %d committees (%d keys, sizes %d-%d) "
+                            "aggregated from a %d-key device registry + one multi_verify"
+                            % (ncom, int(off[-1]), int(np.diff(off).min()), int(np.diff(off).max()), nreg))
         else:
-            rc = L.gbls_multi_verify_partials_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n, seg,
-                                                     1, ptr(d_part), ptr(d_err), st)
-            G.check(rc, "multi_verify_partials_device")
+            nreg = 1_700_000
+            total = args.sets or (1 << 20)
+            n = total // world
+            sks, comp = F.registry(nreg, seed=b"holesky")
+            assert not F.load_registry(comp).any()
+            rng = np.random.default_rng(rank + 5)
+            idx = rng.integers(0, nreg, size=n, dtype=np.uint32)
+            off = None
+            msgs = F.messages(n, b"c5/%d" % rank)
+            sigs = F.sign([sks[int(i)] for i in idx], msgs)
+            rands = F.rands(n, rank + 5)
+            leg.scaling = "strong"
+            leg.workload = ("C5: %d sets in total (%d per GPU), keys drawn uniformly from a %d-key device "
+                            "registry, distinct messages, one multi_verify per GPU" % (total, n, nreg))
+        d_msgs, d_sigs = dbytes(msgs), dbytes(sigs)
+        d_rands = torch.tensor(to_i64(rands), dtype=torch.int64, device=dev)
+        d_idx = dnp(idx) if idx is not None else None
+        d_off = dnp(off) if off is not None else None
+        d_verdict = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        d_part = torch.zeros(576, dtype=torch.uint8, device=dev)
+        d_err = torch.zeros(1, dtype=torch.int32, device=dev)
+        d_parts = torch.zeros(world * 576, dtype=torch.uint8, device=dev)
+        d_errs = torch.zeros(world, dtype=torch.int32, device=dev)
+        seg = G.u32_array([0, n])
+        leg.units = n
+
+        def step():
+            st = cur_stream()
+            pidx = ptr(d_idx) if d_idx is not None else None
+            poff = ptr(d_off) if d_off is not None else None
+            if world == 1:
+                if cfg == "C2":
+                    rc = L.gbls_multi_verify_segments_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n,
+                                                             seg, 1, ptr(d_verdict), st)
+                else:
+                    rc = L.gbls_multi_verify_indexed_segments_device(ptr(d_msgs), ptr(d_sigs), pidx, poff,
+                                                                     ptr(d_rands), n, seg, 1, ptr(d_verdict), st)
+                G.check(rc, "multi_verify device")
+                return
+            if cfg == "C2":
+                rc = L.gbls_multi_verify_partials_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n, seg,
+                                                         1, ptr(d_part), ptr(d_err), st)
+            else:
+                rc = L.gbls_multi_verify_indexed_partials_device(ptr(d_msgs), ptr(d_sigs), pidx, poff, ptr(d_rands),
+                                                                 n, seg, 1, ptr(d_part), ptr(d_err), st)
+            G.check(rc, "multi_verify partials")
             dist.all_gather_into_tensor(d_parts, d_part)
             dist.all_gather_into_tensor(d_errs, d_err)
-            st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-            rc = L.gbls_final_verify_partials_device(ptr(d_parts), ptr(d_errs), world, 1, ptr(d_verdict), st)
-            G.check(rc, "final_verify_partials_device")
+            rc = L.gbls_final_verify_partials_device(ptr(d_parts), ptr(d_errs), world, 1, ptr(d_verdict),
+                                                     cur_stream())
+            G.check(rc, "final_verify_partials")
+
+        def verdict_ok():
+            return int(d_verdict.item()) == G.SUCCESS
+
+        leg.stage_units = lambda s: {"k_ml_leaf": n + 1, "k_ml_reduce": n + 1, "k_lines_S": 1,
+                                     "k_g1_aggregate_idx": getattr(leg, "pks_per_step", n)}.get(s, n)
+    # ------------------------------------------------------------------ C3
+    elif cfg == "C3":
+        m = args.sets or 10_000
+        k = 512
+        sks, comp = F.registry(1 << 16, seed=b"c3-registry")
+        assert not F.load_registry(comp).any()
+        rng = np.random.default_rng(rank + 3)
+        committee = rng.choice(1 << 16, size=k, replace=False).astype(np.uint32)
+        ssum = sum(sks[int(i)] for i in committee) % F.R_ORDER
+        msgs = F.messages(m, b"c3/%d" % rank)
+        sigs = bytearray(F.sign([ssum] * m, msgs))
+        invalid = sorted(rng.choice(m, size=m // 100, replace=False).tolist())
+        wrong = F.sign([(ssum + 1) % F.R_ORDER], msgs[:32])
+        for i in invalid:
+            sigs[192 * i:192 * i + 192] = wrong
+        d_msgs, d_sigs = dbytes(msgs), dbytes(bytes(sigs))
+        d_idx = dnp(np.tile(committee, m))
+        d_off = dnp(np.arange(0, k * m + 1, k, dtype=np.uint32))
+        d_v = torch.full((m,), -1, dtype=torch.int32, device=dev)
+        want = torch.zeros(m, dtype=torch.int32)
+        want[invalid] = G.VERIFY_FAIL
+        leg.units = m
+        leg.metric = "sync-committee fast_aggregate_verify messages/sec (whole node)"
+        leg.unit = "messages/s"
+        leg.workload = ("C3: %d messages per GPU, each fast_aggregate_verify against the same %d-key sync "
+                        "committee (registry indices, aggregated on device every step), 1%% invalid" % (m, k))
+
+        def step():
+            G.check(L.gbls_fast_aggregate_verify_indexed_device(ptr(d_sigs), ptr(d_msgs), ptr(d_idx), ptr(d_off), m,
+                                                                ptr(d_v), cur_stream()), "fav indexed device")
+
+        def verdict_ok():
+            return bool(torch.equal(d_v.cpu(), want))
+
+        leg.stage_units = lambda s: {"k_g1_aggregate_idx": m * k, "k_lines_S": m, "k_ml_leaf": 2 * m,
+                                     "k_ml_reduce": 2 * m}.get(s, m)
+    # ------------------------------------------------------------------ C1 (latency, host ABI)
+    else:
+        return bench_c1(args, L, G, F, np)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if int(d_verdict.item()) != G.SUCCESS:
-        raise SystemExit("verification of the valid batch FAILED (verdict %d)" % int(d_verdict.item()))
+    if not verdict_ok():
+        raise SystemExit("verdicts of the warm-up step are WRONG")
 
     L.gbls_profile_reset()
     L.gbls_profile(1)
@@ -192,7 +309,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     L.gbls_profile(0)
-    ok = int(d_verdict.item()) == G.SUCCESS
+    ok = verdict_ok()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -201,10 +318,10 @@ def main():
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
     if not ok:
-        raise SystemExit("verdict changed during the timed region")
+        raise SystemExit("verdicts changed during the timed region")
 
     # ---- roofline of the dominant kernel (HIP events on the launch stream)
-    nst = 16
+    nst = 32
     ms = (ctypes.c_double * nst)()
     calls = (ctypes.c_uint32 * nst)()
     ns = L.gbls_profile_read(ms, calls, nst)
@@ -215,30 +332,114 @@ def main():
     if dom:
         tot_ms, ncalls = stages[dom]
         avg_s = tot_ms / ncalls * 1e-3
-        units = {"k_ml_leaf": n + 1, "k_ml_reduce": n + 1, "k_lines_S": 1}.get(dom, n)
-        mads = units * W_FPMUL.get(dom, 0) * MAD_PER_FPMUL
+        mads = leg.stage_units(dom) * W_FPMUL.get(dom, 0) * MAD_PER_FPMUL
         ach = mads / avg_s / 1e12
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4),
-                "peak": round(peak / 1e12, 3), "unit": "Tmad64/s", "frac": round(ach / (peak / 1e12), 5) if peak else None,
-                "traffic": pmc_traffic(dom, n), "avg_launch_ms": round(tot_ms / ncalls, 4),
+                "peak": round(peak / 1e12, 3), "unit": "Tmad64/s",
+                "frac": round(ach / (peak / 1e12), 5) if peak else None,
+                "traffic": pmc_traffic(dom, leg.units) if cfg == "C2" else None,
+                "avg_launch_ms": round(tot_ms / ncalls, 4),
                 "stage_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()}}
 
     if rank == 0:
-        value = world * n * args.steps / dt
-        cpu = None if args.no_cpu or world > 1 else cpu_baseline(args.cpu_sample, args.cpu_threads)
-        line = {"metric": "verified BLS signature sets/sec (whole node)", "value": round(value, 1),
-                "unit": "sets/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        value = world * leg.units * args.steps / dt if leg.scaling == "weak" else world * leg.units * args.steps / dt
+        cpu = None
+        if not args.no_cpu and world == 1 and cfg == "C2":
+            cpu = cpu_baseline(args.cpu_sample, args.cpu_threads or cpu_threads())
+        line = {"metric": leg.metric, "value": round(value, 1),
+                "unit": leg.unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
-                "data": "synthetic (interop keys, seeded messages / scalars)",
-                "config": {"workload": "C2: %d single-pubkey sets per GPU, random-scalar multi_verify" % n,
-                           "sets_per_gpu": n, "parallelism": "shard sets, RCCL all-gather of Fp12 partials"
-                           if world > 1 else "1 GPU"},
-                "pairings_per_s": round(world * (n + 1) * args.steps / dt, 1),
+                "scaling": leg.scaling, "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
+                "data": "synthetic (seeded keys, messages and scalars; signed on device)",
+                "config": {"workload": leg.workload, "config": cfg, "units_per_gpu_per_step": leg.units,
+                           "parallelism": "shard sets, RCCL all-gather of Fp12 partials" if world > 1 else "1 GPU"},
                 "roofline": roof, "cpu_baseline": cpu}
+        if cfg in ("C2", "C4", "C5"):
+            line["pairings_per_s"] = round(world * (leg.units + 1) * args.steps / dt, 1)
+        if cfg == "C4":
+            line["pks_aggregated_per_s"] = round(world * leg.pks_per_step * args.steps / dt, 1)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_c1(args, L, G, F, np):
+    """C1: a mainnet-shaped block's signature sets (1 proposer + 1 RANDAO + 128 aggregate
+    attestations of ~512 registry keys + a 512-key sync aggregate = 131 sets) through the
+    host-pointer ABI exactly as MultiVerifier::finish would call it (G2 decompression of
+    the 131 signatures, then one indexed multi_verify): per-call latency, PCIe included.
+    Also: 64-set gossip batches (p2p/src/attestation_verifier.rs:37), serial and from 16
+    concurrent threads (the node's verifier tasks)."""
+    import threading
+    nreg = 1 << 20
+    sks, comp = F.registry(nreg, seed=b"c1-registry")
+    assert not F.load_registry(comp).any()
+    rng = np.random.default_rng(1)
+    sizes = [1, 1] + [512] * 128 + [512]
+    idx = np.concatenate([rng.choice(nreg, size=s, replace=False) for s in sizes]).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    n = len(sizes)
+    msgs = F.messages(n, b"c1")
+    sigs, _ = F.committee_signatures(sks, idx, off, msgs)
+    comp_sigs = ctypes.create_string_buffer(96 * n)
+    G.check(L.gbls_g2_compress(sigs, n, comp_sigs), "compress")
+    rands = F.rands(n, 1)
+
+    def finish():
+        dec = ctypes.create_string_buffer(192 * n)
+        st = G.i32_array(n)
+        G.check(L.gbls_g2_decompress(comp_sigs, n, dec, st), "decompress")
+        assert all(st[i] == 0 for i in range(n))
+        return L.gbls_multi_verify_indexed(msgs, dec, idx.ctypes.data_as(ctypes.c_void_p),
+                                           off.ctypes.data_as(ctypes.c_void_p),
+                                           (ctypes.c_uint64 * n)(*rands), n)
+
+    for _ in range(args.warmup):
+        assert finish() == G.SUCCESS
+    lat = []
+    for _ in range(args.steps):
+        t = time.perf_counter()
+        assert finish() == G.SUCCESS
+        lat.append(time.perf_counter() - t)
+    # gossip: 64 single-key sets per call
+    gm, gs, gp, gr = F.c2_batch(64, seed=64)
+    r64 = (ctypes.c_uint64 * 64)(*gr)
+    glat = []
+    for _ in range(args.steps):
+        t = time.perf_counter()
+        assert L.gbls_multi_verify(gm, gs, gp, r64, 64) == G.SUCCESS
+        glat.append(time.perf_counter() - t)
+    nthr, per = 16, max(4, args.steps)
+    errs = []
+
+    def worker():
+        for _ in range(per):
+            if L.gbls_multi_verify(gm, gs, gp, r64, 64) != G.SUCCESS:
+                errs.append(1)
+
+    ths = [threading.Thread(target=worker) for _ in range(nthr)]
+    t = time.perf_counter()
+    for x in ths:
+        x.start()
+    for x in ths:
+        x.join()
+    conc = time.perf_counter() - t
+    assert not errs
+    lat.sort()
+    glat.sort()
+    line = {"metric": "MultiVerifier::finish latency, mainnet-shaped block (C1)", "value": round(lat[len(lat) // 2] * 1e3, 3),
+            "unit": "ms (p50)", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(sum(lat) / len(lat) * 1e3, 3), "higher_is_better": False, "scaling": "n/a",
+            "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
+            "data": "synthetic (seeded registry, committees and messages)",
+            "config": {"workload": "C1: %d sets (%d keys aggregated from the registry), host pointers, PCIe included"
+                                   % (n, int(off[-1])), "config": "C1"},
+            "p99_ms": round(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3, 3),
+            "gossip64": {"p50_ms": round(glat[len(glat) // 2] * 1e3, 3),
+                         "p99_ms": round(glat[min(len(glat) - 1, int(len(glat) * 0.99))] * 1e3, 3),
+                         "concurrent_16_threads_sets_per_s": round(nthr * per * 64 / conc, 1)},
+            "roofline": None, "cpu_baseline": None}
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -32,6 +32,7 @@ EXPORTS = [
     "gbls_init",
     "gbls_last_error",
     "gbls_version",
+    "gbls_device_count",
     "gbls_g1_decompress",
     "gbls_g2_decompress",
     "gbls_g2_validate",
@@ -40,6 +41,16 @@ EXPORTS = [
     "gbls_g1_aggregate",
     "gbls_g1_aggregate_segments",
     "gbls_g2_aggregate",
+    "gbls_g2_aggregate_segments",
+    "gbls_registry_set",
+    "gbls_registry_size",
+    "gbls_g1_aggregate_indexed",
+    "gbls_fast_aggregate_verify_indexed",
+    "gbls_multi_verify_indexed",
+    "gbls_multi_verify_bisect",
+    "gbls_multi_verify_indexed_segments_device",
+    "gbls_fast_aggregate_verify_indexed_device",
+    "gbls_multi_verify_indexed_partials_device",
     "gbls_verify",
     "gbls_fast_aggregate_verify",
     "gbls_aggregate_verify_batch",
@@ -86,6 +97,7 @@ def load_library():
                 "gbls_init": (_c.c_int, [_c.c_uint32, _c.c_uint32]),
                 "gbls_last_error": (_c.c_int, []),
                 "gbls_version": (_c.c_char_p, []),
+                "gbls_device_count": (_c.c_int, []),
                 "gbls_g1_decompress": (_c.c_int, [_vp, _sz, _c.c_int, _vp, _vp]),
                 "gbls_g2_decompress": (_c.c_int, [_vp, _sz, _vp, _vp]),
                 "gbls_g2_validate": (_c.c_int, [_vp, _sz, _vp]),
@@ -94,6 +106,18 @@ def load_library():
                 "gbls_g1_aggregate": (_c.c_int, [_vp, _sz, _vp]),
                 "gbls_g1_aggregate_segments": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
                 "gbls_g2_aggregate": (_c.c_int, [_vp, _sz, _vp]),
+                "gbls_g2_aggregate_segments": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
+                "gbls_registry_set": (_c.c_int, [_sz, _vp, _sz, _vp]),
+                "gbls_registry_size": (_sz, []),
+                "gbls_g1_aggregate_indexed": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
+                "gbls_fast_aggregate_verify_indexed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+                "gbls_multi_verify_indexed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
+                "gbls_multi_verify_bisect": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+                "gbls_fast_aggregate_verify_indexed_device": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+                "gbls_multi_verify_indexed_partials_device": (
+                    _c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp]),
+                "gbls_multi_verify_indexed_segments_device": (
+                    _c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp]),
                 "gbls_verify": (_c.c_int, [_vp, _vp, _sz, _vp]),
                 "gbls_fast_aggregate_verify": (_c.c_int, [_vp, _vp, _sz, _vp, _sz]),
                 "gbls_aggregate_verify_batch": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
@@ -122,14 +146,15 @@ def load_library():
     return _lib
 
 
-def lib():
-    """The library with the device initialised (raises if no gfx950 device)."""
+def lib(device_mask: int = 0, flags: int = 0):
+    """The library with the device initialised (raises if no gfx950 device).  The first
+    call's device_mask / flags configure the engine (gbls_init is idempotent)."""
     global _ready
     L = load_library()
     if not _ready:
         with _lock:
             if not _ready:
-                if L.gbls_init(0, 0) != SUCCESS:
+                if L.gbls_init(device_mask, flags) != SUCCESS:
                     raise EngineUnavailable(
                         f"gbls_init failed (error {L.gbls_last_error()}): no usable gfx950 device")
                 _ready = True

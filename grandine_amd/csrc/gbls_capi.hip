@@ -2,15 +2,31 @@
 // (k_*.hip).  Entry points, their reference counterparts and semantics are documented
 // in include/grandine_bls_gpu.h.
 //
-// Concurrency model: a process-wide engine (one HIP device, one stream, grow-only
-// device workspaces) guarded by a mutex; callers from many threads are serialised
-// onto the stream.  Every failure is fail-closed (VERIFY_FAIL + gbls_last_error).
+// Concurrency model (rayon workers, the de-low executor, the block
+// verification pool and fork-choice workers all call in concurrently):
+//   * one Device per GPU of gbls_init's device mask (optionally several engines per
+//     GPU, for tests of the multi-device paths on one card);
+//   * every call leases a Ctx -- streams, events, grow-only workspaces, a pinned
+//     staging buffer -- from its device's pool, so concurrent callers run side by side
+//     on separate streams with no shared scratch;
+//   * a Ctx is handed to the next caller only behind a GPU-side wait on the completion
+//     event of its previous call (device-pointer calls return before their kernels
+//     finish), and its buffers are only regrown after a host wait on that event;
+//   * host-pointer calls shard big batches over the devices: whole segments per device,
+//     or, for one large batch, per-device Miller partials combined by one final
+//     exponentiation.
+// Every failure is fail-closed: GBLS_VERIFY_FAIL (verdict arrays filled with it first)
+// plus a thread-local gbls_last_error code.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <vector>
 
 #include "../../include/grandine_bls_gpu.h"
@@ -24,7 +40,24 @@ static_assert(sizeof(fp12) == sizeof(gbls_fp12), "fp12 layout");
 
 namespace {
 
+constexpr int FAILED = GBLS_VERIFY_FAIL;  // engine/driver failure return (fail closed)
+constexpr size_t kShardMinSets = 1024;     // per device, before a batch is split
+constexpr int kMaxCtxPerDevice = 64;
+
 thread_local int t_last_error = GBLS_ERR_NONE;
+
+bool fail(int code) {
+  t_last_error = code;
+  return false;
+}
+
+#define HIPCHK(x)                  \
+  do {                             \
+    if ((x) != hipSuccess) {       \
+      t_last_error = GBLS_ERR_HIP; \
+      return false;                \
+    }                              \
+  } while (0)
 
 struct Buf {
   void *p = nullptr;
@@ -48,24 +81,16 @@ struct Buf {
 // ---- optional per-stage timing (HIP events on the launch stream), for bench.py
 enum Stage {
   S_H2C_FIELD, S_H2C_MAP, S_H2C_CLEAR, S_G1MUL, S_G2MUL, S_G2SUM, S_LINES, S_LINES_S, S_ML_LEAF,
-  S_ML_REDUCE, S_ML_HORNER, S_FINAL, S_COUNT
+  S_ML_REDUCE, S_ML_HORNER, S_FINAL, S_PK_GATHER, S_COUNT
 };
 const char *kStageNames[S_COUNT] = {"k_h2c_field", "k_h2c_map",   "k_h2c_clear", "k_mv_g1mul",
                                     "k_mv_g2mul",  "k_g2sum",      "k_lines",     "k_lines_S",
-                                    "k_ml_leaf",   "k_ml_reduce",  "k_ml_horner", "k_final_verdict"};
+                                    "k_ml_leaf",   "k_ml_reduce",  "k_ml_horner", "k_final_verdict",
+                                    "k_g1_aggregate_idx"};
 
-struct Engine {
+struct Prof {
   std::mutex mu;
-  bool ready = false;
-  int device = -1;
-  hipStream_t stream = nullptr;
-  hipStream_t side1 = nullptr, side2 = nullptr;  // fork/join streams of the pipeline
-  hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr;
-  // workspaces
-  Buf in0, in1, in2, in3, in4, in5, in6, U, Q, H, P, R, gpart, lines, V0, V1, tab, segoff, part,
-      err, out0, out1;
-  // profiling
-  bool prof = false;
+  std::atomic<bool> on{false};
   struct Rec {
     int stage;
     hipEvent_t a, b;
@@ -73,89 +98,254 @@ struct Engine {
   std::vector<Rec> pending;
   double ms[S_COUNT] = {0};
   uint32_t calls[S_COUNT] = {0};
-} g;
-
-bool fail(int code) {
-  t_last_error = code;
-  return false;
-}
-
-#define HIPCHK(x)                  \
-  do {                             \
-    if ((x) != hipSuccess) {       \
-      t_last_error = GBLS_ERR_HIP; \
-      return false;                \
-    }                              \
-  } while (0)
+} prof;
 
 struct StageTimer {  // RAII: events around one stage's launches when profiling
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t st;
   int stage;
   StageTimer(int s, hipStream_t stream) : st(stream), stage(s) {
-    if (!g.prof) return;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+    if (!prof.on.load(std::memory_order_relaxed)) return;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+      a = b = nullptr;
+      return;
+    }
     (void)hipEventRecord(a, st);
   }
   ~StageTimer() {
-    if (!g.prof || !a || !b) return;
+    if (!a || !b) return;
     (void)hipEventRecord(b, st);
-    g.pending.push_back({stage, a, b});
+    std::lock_guard<std::mutex> lk(prof.mu);
+    prof.pending.push_back({stage, a, b});
   }
 };
 
-bool engine_init_locked(uint32_t device_mask) {
-  if (g.ready) return true;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GBLS_ERR_NO_DEVICE);
-  int dev = 0;
-  if (device_mask) {
-    while (dev < 32 && !((device_mask >> dev) & 1)) dev++;
-  } else {
-    (void)hipGetDevice(&dev);
-  }
-  if (dev >= ndev) return fail(GBLS_ERR_NO_DEVICE);
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(GBLS_ERR_NO_DEVICE);
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return fail(GBLS_ERR_NO_DEVICE);
-  HIPCHK(hipSetDevice(dev));
-  HIPCHK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&g.side1, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&g.side2, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&g.ev_fork, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&g.ev_side1, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&g.ev_side2, hipEventDisableTiming));
-  g.device = dev;
-  g.ready = true;
-  return true;
-}
+// ---------------------------------------------------------------- per-call context
+struct Ctx {
+  int hipdev = -1;
+  hipStream_t own = nullptr, side1 = nullptr, side2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_done = nullptr,
+             ev_upl = nullptr;
+  bool done_pending = false, upl_pending = false;
+  bool active = false;                // a call holds the lease and has begun
+  hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
+  bool used = false;                  // last_stream is meaningful
+  hipStream_t last_stream = nullptr;  // main stream of the previous call
+  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, gpart, lines, V0, V1, tab, part, err, out0,
+      out1, pks, pre;
+  void *stage = nullptr;
+  size_t stage_cap = 0, stage_used = 0;
+  std::vector<uint32_t> host_tab;  // table assembly, reused across calls
 
-bool ensure_ready() {
-  if (g.ready) {
-    (void)hipSetDevice(g.device);
+  bool init(int dev) {
+    hipdev = dev;
+    HIPCHK(hipSetDevice(dev));
+    HIPCHK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&side1, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&side2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_side1, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_side2, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_upl, hipEventDisableTiming));
     return true;
   }
-  return engine_init_locked(0);
+  // the call's main stream waits (on the GPU) for the previous call on this context;
+  // the staging buffer is recycled once the previous call's uploads have landed
+  bool begin(hipStream_t st) {
+    cur = st;
+    active = true;
+    if (upl_pending) {
+      HIPCHK(hipEventSynchronize(ev_upl));
+      upl_pending = false;
+    }
+    stage_used = 0;
+    if (done_pending) HIPCHK(hipStreamWaitEvent(st, ev_done, 0));
+    return true;
+  }
+  // true when the previous call on this context has finished on the GPU
+  bool idle_on_gpu() {
+    if (!done_pending) return true;
+    if (hipEventQuery(ev_done) != hipSuccess) return false;
+    done_pending = false;
+    return true;
+  }
+  // host wait for the previous call (before buffers are reallocated)
+  bool drain() {
+    if (done_pending) {
+      HIPCHK(hipEventSynchronize(ev_done));
+      done_pending = false;
+    }
+    return true;
+  }
+  bool ensure(Buf &b, size_t bytes) {
+    if (bytes <= b.cap) return true;
+    if (!drain()) return false;
+    // an in-flight stage of THIS call may still read the old buffer
+    if (active) HIPCHK(hipStreamSynchronize(cur));
+    return b.ensure(bytes) || fail(GBLS_ERR_HIP);
+  }
+  // bump allocation in the pinned staging buffer (per call); regrowing waits for the
+  // uploads of this call that still read it
+  void *staging(size_t bytes) {
+    size_t need = (bytes + 255) & ~(size_t)255;
+    if (stage_used + need > stage_cap) {
+      if (upl_pending) {
+        if (hipEventSynchronize(ev_upl) != hipSuccess) return nullptr;
+        upl_pending = false;
+      }
+      if (need > stage_cap) {
+        if (stage) (void)hipHostFree(stage);
+        stage = nullptr;
+        stage_cap = 0;
+        size_t want = std::max<size_t>(need * 2, 1 << 20);
+        if (hipHostMalloc(&stage, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+        stage_cap = want;
+      }
+      stage_used = 0;
+    }
+    void *p = static_cast<uint8_t *>(stage) + stage_used;
+    stage_used += need;
+    return p;
+  }
+  bool upload_staged(Buf &dst, const void *host, size_t bytes, hipStream_t st) {
+    if (!ensure(dst, bytes + 16)) return false;
+    if (!bytes) return true;
+    void *s = staging(bytes);
+    if (!s) return fail(GBLS_ERR_HIP);
+    std::memcpy(s, host, bytes);
+    HIPCHK(hipMemcpyAsync(dst.p, s, bytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ev_upl, st));
+    upl_pending = true;
+    return true;
+  }
+};
+
+struct Device {
+  int hipdev = -1;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Ctx *> idle;
+  std::vector<std::unique_ptr<Ctx>> all;
+  Buf reg;  // validator registry (replica), guarded by Engine::reg_mu
+};
+
+struct Engine {
+  std::mutex mu;
+  std::atomic<bool> ready{false};
+  std::vector<std::unique_ptr<Device>> devs;
+  std::atomic<uint32_t> rr{0};
+  std::shared_mutex reg_mu;
+  size_t reg_n = 0;
+} g;
+
+// RAII lease of a context of one device: the idle context last used on the caller's
+// stream (stream order makes its reuse free), else an idle context whose previous call
+// has finished on the GPU, else a new one (up to kMaxCtxPerDevice), else the least
+// recently used idle context (its reuse is ordered behind its previous call on the GPU)
+class Lease {
+ public:
+  Lease(Device &d, bool affine, hipStream_t stream) : d_(d) {
+    std::unique_lock<std::mutex> lk(d.mu);
+    for (;;) {
+      for (size_t i = 0; affine && !c_ && i < d.idle.size(); i++)
+        if (d.idle[i]->used && d.idle[i]->last_stream == stream) {
+          c_ = d.idle[i];
+          d.idle.erase(d.idle.begin() + i);
+        }
+      for (size_t i = 0; !c_ && i < d.idle.size(); i++)
+        if (d.idle[i]->idle_on_gpu()) {
+          c_ = d.idle[i];
+          d.idle.erase(d.idle.begin() + i);
+        }
+      if (!c_ && (int)d.all.size() < kMaxCtxPerDevice) {
+        d.all.emplace_back(new Ctx());
+        c_ = d.all.back().get();
+        fresh_ = true;
+      }
+      if (!c_ && !d.idle.empty()) {
+        c_ = d.idle.front();
+        d.idle.erase(d.idle.begin());
+      }
+      if (c_) break;
+      d.cv.wait(lk);  // every context is leased: wait for one to come back
+    }
+    lk.unlock();
+    ok_ = fresh_ ? c_->init(d.hipdev) : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
+  }
+  explicit Lease(Device &d) : Lease(d, false, nullptr) {}
+  ~Lease() {
+    if (c_->active) {
+      if (hipEventRecord(c_->ev_done, c_->cur) == hipSuccess) c_->done_pending = true;
+      c_->last_stream = c_->cur;
+      c_->used = true;
+      c_->active = false;
+      c_->cur = nullptr;
+    }
+    {
+      std::lock_guard<std::mutex> lk(d_.mu);
+      d_.idle.push_back(c_);
+    }
+    d_.cv.notify_one();
+  }
+  bool ok() const { return ok_; }
+  Ctx &operator*() { return *c_; }
+  Ctx *operator->() { return c_; }
+
+ private:
+  Device &d_;
+  Ctx *c_ = nullptr;
+  bool fresh_ = false, ok_ = false;
+};
+
+bool engine_init(uint32_t device_mask, uint32_t flags) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (g.ready.load()) return true;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GBLS_ERR_NO_DEVICE);
+  std::vector<int> ids;
+  if (device_mask) {
+    for (int d = 0; d < 32 && d < ndev; d++)
+      if ((device_mask >> d) & 1) ids.push_back(d);
+  } else {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    ids.push_back(cur);
+  }
+  if (ids.empty()) return fail(GBLS_ERR_NO_DEVICE);
+  int replicas = (int)(flags & 0xffu);
+  if (replicas < 1) replicas = 1;
+  for (int id : ids) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, id) != hipSuccess) return fail(GBLS_ERR_NO_DEVICE);
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return fail(GBLS_ERR_NO_DEVICE);
+    for (int r = 0; r < replicas; r++) {
+      g.devs.emplace_back(new Device());
+      g.devs.back()->hipdev = id;
+    }
+  }
+  g.ready.store(true);
+  return true;
 }
 
-template <class T>
-bool upload(Buf &b, const T *host, size_t count, hipStream_t st) {
-  if (!b.ensure(count * sizeof(T) + 16)) return fail(GBLS_ERR_HIP);
-  if (count) HIPCHK(hipMemcpyAsync(b.p, host, count * sizeof(T), hipMemcpyHostToDevice, st));
-  return true;
+bool ensure_ready() { return g.ready.load() || engine_init(0, 0); }
+
+// the engine device(s) of the calling thread's current HIP device (device-pointer calls)
+Device *current_device() {
+  int id = 0;
+  if (hipGetDevice(&id) != hipSuccess) return nullptr;
+  std::vector<Device *> cand;
+  for (auto &d : g.devs)
+    if (d->hipdev == id) cand.push_back(d.get());
+  if (cand.empty()) return nullptr;
+  return cand[g.rr.fetch_add(1) % cand.size()];
 }
-template <class T>
-bool upload(Buf &b, const T *host, size_t count) {
-  return upload(b, host, count, g.stream);
-}
-template <class T>
-bool download(T *host, const Buf &b, size_t count) {
-  if (count) HIPCHK(hipMemcpyAsync(host, b.p, count * sizeof(T), hipMemcpyDeviceToHost, g.stream));
-  return true;
-}
-bool sync() {
-  HIPCHK(hipStreamSynchronize(g.stream));
-  HIPCHK(hipGetLastError());
+Device &pick_device() { return *g.devs[g.rr.fetch_add(1) % g.devs.size()]; }
+
+bool valid_offsets(const uint32_t *off, size_t nseg, size_t n) {
+  if (!off || off[0] != 0 || off[nseg] != n) return false;
+  for (size_t s = 0; s < nseg; s++)
+    if (off[s + 1] < off[s]) return false;
   return true;
 }
 
@@ -163,21 +353,24 @@ bool sync() {
 // Sets [0, n) grouped in segments by seg_off (HOST array, nseg + 1 entries); per segment
 // a Miller partial (no final exponentiation) and an error flag.  rands == nullptr
 // means r_i = 1 (single checks); pre[i] != 0 marks a set that failed a pre-check.
-bool pipeline_partials(const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
+bool pipeline_partials(Ctx &c, const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
                        const g1a *pks, const uint64_t *rands, const int32_t *pre, size_t n,
-                       const uint32_t *seg_off, size_t nseg, fp12 *partials, int32_t *seg_err,
-                       hipStream_t st) {
+                       const uint32_t *seg_off, size_t nseg, int empty_is_error, fp12 *partials,
+                       int32_t *seg_err, hipStream_t st) {
   const size_t np = n + nseg;
-  // ---- host tables, one upload: [couples][g2 chunks][seg_chunk][reduction levels]
-  std::vector<uint32_t> tab;
+  // ---- host tables, one staged upload:
+  //   [couples][g2 chunks][seg_chunk][reduction levels][seg_off]
+  std::vector<uint32_t> &tab = c.host_tab;
+  tab.clear();
   std::vector<uint32_t> cnt(nseg);
   for (size_t s = 0; s < nseg; s++) {  // level-0 couples of each segment's pair list
-    std::vector<uint32_t> list;
-    for (uint32_t i = seg_off[s]; i < seg_off[s + 1]; i++) list.push_back(i);
-    list.push_back((uint32_t)(n + s));
-    for (size_t j = 0; j < list.size(); j += 2) {
-      tab.push_back(list[j]);
-      tab.push_back(j + 1 < list.size() ? list[j + 1] : NONE);
+    uint32_t b = seg_off[s], e = seg_off[s + 1];
+    uint32_t len = e - b + 1;  // + the segment's (-g1, S) pair at n + s
+    for (uint32_t j = 0; j < len; j += 2) {
+      uint32_t x = j < e - b ? b + j : (uint32_t)(n + s);
+      uint32_t y = j + 1 < len ? (j + 1 < e - b ? b + j + 1 : (uint32_t)(n + s)) : NONE;
+      tab.push_back(x);
+      tab.push_back(y);
       cnt[s]++;
     }
   }
@@ -213,85 +406,87 @@ bool pipeline_partials(const uint8_t *msgs, const uint32_t *msg_off, const g2a *
     size_t in_base = 0;
     std::vector<uint32_t> next(nseg);
     for (size_t s = 0; s < nseg; s++) {
-      uint32_t c = cnt[s];
-      for (uint32_t q = 0; q < c; q += 4) {
+      uint32_t k = cnt[s];
+      for (uint32_t q = 0; q < k; q += 4) {
         tab.push_back((uint32_t)(in_base + q));
-        tab.push_back(std::min<uint32_t>(4, c - q));
+        tab.push_back(std::min<uint32_t>(4, k - q));
         next[s]++;
       }
-      in_base += c;
+      in_base += k;
     }
     L.nout = (tab.size() - L.tab_off) / 2;
     levels.push_back(L);
     cnt = next;
     cur_n = L.nout;
   }
+  const size_t segoff_at = tab.size();
+  tab.insert(tab.end(), seg_off, seg_off + nseg + 1);
   // ---- workspaces
   const size_t line_words = (size_t)np * ML_EVENTS * 72;
   size_t v1_n = 1, v0_n = ncouple;
   for (size_t l = 0; l < levels.size(); l++)
     (l & 1 ? v0_n : v1_n) = std::max(l & 1 ? v0_n : v1_n, levels[l].nout);
-  if (!g.U.ensure(2 * n * sizeof(fp2)) || !g.Q.ensure(2 * n * sizeof(g2j)) ||
-      !g.H.ensure(np * sizeof(g2a)) || !g.P.ensure(np * sizeof(g1a)) ||
-      !g.R.ensure(2 * n * sizeof(g2j) + 16) || !g.gpart.ensure(nchunks * (sizeof(g2j) + 4)) ||
-      !g.lines.ensure(line_words * 4) || !g.V0.ensure(ML_EVENTS * v0_n * sizeof(fp12)) ||
-      !g.V1.ensure(ML_EVENTS * v1_n * sizeof(fp12)) || !g.segoff.ensure((nseg + 1) * 4))
-    return fail(GBLS_ERR_HIP);
-  if (!upload(g.tab, tab.data(), tab.size(), st)) return false;
-  HIPCHK(hipMemcpyAsync(g.segoff.p, seg_off, (nseg + 1) * 4, hipMemcpyHostToDevice, st));
+  if (!c.ensure(c.U, 2 * n * sizeof(fp2) + 16) || !c.ensure(c.Q, 2 * n * sizeof(g2j) + 16) ||
+      !c.ensure(c.H, np * sizeof(g2a)) || !c.ensure(c.P, np * sizeof(g1a)) ||
+      !c.ensure(c.R, 2 * n * sizeof(g2j) + 16) ||
+      !c.ensure(c.gpart, nchunks * (sizeof(g2j) + 4)) || !c.ensure(c.lines, line_words * 4) ||
+      !c.ensure(c.V0, ML_EVENTS * v0_n * sizeof(fp12)) ||
+      !c.ensure(c.V1, ML_EVENTS * v1_n * sizeof(fp12)))
+    return false;
+  if (!c.upload_staged(c.tab, tab.data(), tab.size() * 4, st)) return false;
   const uint32_t N = (uint32_t)n, NP = (uint32_t)np, NS = (uint32_t)nseg;
-  const uint32_t *T = g.tab.as<uint32_t>();
-  g2j *gpart = g.gpart.as<g2j>();
+  const uint32_t *T = c.tab.as<uint32_t>();
+  g2j *gpart = c.gpart.as<g2j>();
   int32_t *gpart_err = reinterpret_cast<int32_t *>(gpart + nchunks);
   // ---- fork: side stream 1 = G1 scalar products, side stream 2 = G2 sum + its lines,
   // main stream = hash_to_G2 + the sets' lines; join before the Miller tree.
-  HIPCHK(hipEventRecord(g.ev_fork, st));
-  HIPCHK(hipStreamWaitEvent(g.side1, g.ev_fork, 0));
-  HIPCHK(hipStreamWaitEvent(g.side2, g.ev_fork, 0));
+  HIPCHK(hipEventRecord(c.ev_fork, st));
+  HIPCHK(hipStreamWaitEvent(c.side1, c.ev_fork, 0));
+  HIPCHK(hipStreamWaitEvent(c.side2, c.ev_fork, 0));
   {
-    StageTimer t(S_G1MUL, g.side1);
-    launch_mv_g1mul(g.side1, pks, rands, N, g.P.as<g1a>());
+    StageTimer t(S_G1MUL, c.side1);
+    launch_mv_g1mul(c.side1, pks, rands, N, c.P.as<g1a>());
   }
   {
-    StageTimer t(S_G2MUL, g.side2);
-    launch_mv_g2mul(g.side2, sigs, rands, N, g.R.as<g2j>());
+    StageTimer t(S_G2MUL, c.side2);
+    launch_mv_g2mul(c.side2, sigs, rands, N, c.R.as<g2j>());
   }
   {
-    StageTimer t(S_G2SUM, g.side2);
-    launch_g2sum(g.side2, g.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
-                 g.segoff.as<uint32_t>(), NS, N, pks, pre, gpart, gpart_err, g.P.as<g1a>(),
-                 g.H.as<g2a>(), seg_err);
+    StageTimer t(S_G2SUM, c.side2);
+    launch_g2sum(c.side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
+                 T + segoff_at, NS, N, pks, rands, pre, empty_is_error, gpart, gpart_err,
+                 c.P.as<g1a>(), c.H.as<g2a>(), seg_err);
   }
   {
-    StageTimer t(S_LINES_S, g.side2);
-    launch_lines(g.side2, g.H.as<g2a>(), N, NS, NP, g.lines.as<uint32_t>());
+    StageTimer t(S_LINES_S, c.side2);
+    launch_lines(c.side2, c.H.as<g2a>(), N, NS, NP, c.lines.as<uint32_t>());
   }
   {
     StageTimer t(S_H2C_FIELD, st);
-    launch_h2c_field(st, msgs, msg_off, N, nullptr, 0, g.U.as<fp2>());
+    launch_h2c_field(st, msgs, msg_off, N, nullptr, 0, c.U.as<fp2>());
   }
   {
     StageTimer t(S_H2C_MAP, st);
-    launch_h2c_map(st, g.U.as<fp2>(), 2 * N, g.Q.as<g2j>());
+    launch_h2c_map(st, c.U.as<fp2>(), 2 * N, c.Q.as<g2j>());
   }
   {
     StageTimer t(S_H2C_CLEAR, st);
-    launch_h2c_clear(st, g.Q.as<g2j>(), N, g.H.as<g2a>());
+    launch_h2c_clear(st, c.Q.as<g2j>(), N, c.H.as<g2a>());
   }
   {
     StageTimer t(S_LINES, st);
-    launch_lines(st, g.H.as<g2a>(), 0, N, NP, g.lines.as<uint32_t>());
+    launch_lines(st, c.H.as<g2a>(), 0, N, NP, c.lines.as<uint32_t>());
   }
-  HIPCHK(hipEventRecord(g.ev_side1, g.side1));
-  HIPCHK(hipEventRecord(g.ev_side2, g.side2));
-  HIPCHK(hipStreamWaitEvent(st, g.ev_side1, 0));
-  HIPCHK(hipStreamWaitEvent(st, g.ev_side2, 0));
+  HIPCHK(hipEventRecord(c.ev_side1, c.side1));
+  HIPCHK(hipEventRecord(c.ev_side2, c.side2));
+  HIPCHK(hipStreamWaitEvent(st, c.ev_side1, 0));
+  HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
   {
     StageTimer t(S_ML_LEAF, st);
-    launch_ml_leaf(st, g.lines.as<uint32_t>(), NP, g.P.as<g1a>(), T, (uint32_t)ncouple,
-                   g.V0.as<fp12>());
+    launch_ml_leaf(st, c.lines.as<uint32_t>(), NP, c.P.as<g1a>(), T, (uint32_t)ncouple,
+                   c.V0.as<fp12>());
   }
-  fp12 *cur = g.V0.as<fp12>(), *other = g.V1.as<fp12>();
+  fp12 *cur = c.V0.as<fp12>(), *other = c.V1.as<fp12>();
   {
     StageTimer t(S_ML_REDUCE, st);
     for (const Level &L : levels) {
@@ -316,116 +511,408 @@ bool pipeline_final(const fp12 *partials, const int32_t *err, size_t nparts, siz
   return true;
 }
 
-bool pipeline_verdicts(const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
+bool pipeline_verdicts(Ctx &c, const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
                        const g1a *pks, const uint64_t *rands, const int32_t *pre, size_t n,
                        const uint32_t *seg_off, size_t nseg, int32_t *verdicts, hipStream_t st) {
-  if (!g.part.ensure(nseg * sizeof(fp12)) || !g.err.ensure(nseg * sizeof(int32_t)))
-    return fail(GBLS_ERR_HIP);
-  return pipeline_partials(msgs, msg_off, sigs, pks, rands, pre, n, seg_off, nseg,
-                           g.part.as<fp12>(), g.err.as<int32_t>(), st) &&
-         pipeline_final(g.part.as<fp12>(), g.err.as<int32_t>(), 1, nseg, verdicts, st);
+  if (!c.ensure(c.part, nseg * sizeof(fp12)) || !c.ensure(c.err, nseg * sizeof(int32_t) + 16))
+    return false;
+  return pipeline_partials(c, msgs, msg_off, sigs, pks, rands, pre, n, seg_off, nseg, 1,
+                           c.part.as<fp12>(), c.err.as<int32_t>(), st) &&
+         pipeline_final(c.part.as<fp12>(), c.err.as<int32_t>(), 1, nseg, verdicts, st);
 }
 
-std::vector<uint32_t> identity_offsets(size_t m) {
-  std::vector<uint32_t> v(m + 1);
-  for (size_t i = 0; i <= m; i++) v[i] = (uint32_t)i;
-  return v;
+// ----- where a batch's public keys come from
+struct PkSource {
+  const g1a *pts = nullptr;       // one point per set, or
+  const uint32_t *idx = nullptr;  // registry indices: one per set (off == nullptr), or
+  const uint32_t *off = nullptr;  // the sum of idx[off[i] .. off[i+1]) per set
+};
+
+// Resolve a DEVICE-side key source into per-set affine keys (+ pre flags) on the device.
+// The caller holds the registry lock (shared) while it enqueues.
+bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t st,
+                 const g1a **pks, const int32_t **pre) {
+  *pre = nullptr;
+  if (src.pts || n == 0) {
+    *pks = src.pts;
+    return true;
+  }
+  if (!src.idx) return fail(GBLS_ERR_ARG);
+  if (!c.ensure(c.pks, n * sizeof(g1a)) || !c.ensure(c.pre, n * sizeof(int32_t))) return false;
+  StageTimer t(S_PK_GATHER, st);
+  const g1a *reg = d.reg.as<g1a>();
+  if (src.off)
+    launch_g1_aggregate_idx(st, reg, (uint32_t)g.reg_n, src.idx, src.off, (uint32_t)n,
+                            c.pks.as<g1a>(), c.pre.as<int32_t>());
+  else
+    launch_g1_gather_idx(st, reg, (uint32_t)g.reg_n, src.idx, (uint32_t)n, c.pks.as<g1a>(),
+                         c.pre.as<int32_t>());
+  *pks = c.pks.as<g1a>();
+  *pre = c.pre.as<int32_t>();
+  return true;
+}
+
+// Upload a HOST key source for sets [b, e) and resolve it on the device.
+bool upload_pks(Ctx &c, Device &d, const PkSource &host, size_t b, size_t e, hipStream_t st,
+                const g1a **pks, const int32_t **pre) {
+  size_t n = e - b;
+  PkSource dev;
+  if (host.pts) {
+    if (!c.upload_staged(c.in2, host.pts + b, n * sizeof(g1a), st)) return false;
+    dev.pts = c.in2.as<g1a>();
+  } else if (host.off) {
+    uint32_t base = host.off[b], cnt = host.off[e] - base;
+    std::vector<uint32_t> off(n + 1);
+    for (size_t i = 0; i <= n; i++) off[i] = host.off[b + i] - base;
+    if (!c.upload_staged(c.in2, host.idx + base, (size_t)cnt * 4, st) ||
+        !c.upload_staged(c.in5, off.data(), (n + 1) * 4, st))
+      return false;
+    dev.idx = c.in2.as<uint32_t>();
+    dev.off = c.in5.as<uint32_t>();
+  } else if (host.idx) {
+    if (!c.upload_staged(c.in2, host.idx + b, n * 4, st)) return false;
+    dev.idx = c.in2.as<uint32_t>();
+  } else {
+    return fail(GBLS_ERR_ARG);
+  }
+  return resolve_pks(c, d, dev, n, st, pks, pre);
+}
+
+// One device: host batch [sets b..e) in segments seg (rebased, host) -> per-segment
+// verdicts (host) when `verdicts`, or else the Miller partial + error flag of the single
+// segment into part_host / err_host.  Enqueues only; the caller synchronises `c.own`.
+bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
+                        const PkSource &src, const uint64_t *rands, size_t b, size_t e,
+                        const uint32_t *seg, size_t nseg, int32_t *verdicts, void *part_host,
+                        int32_t *err_host) {
+  hipStream_t st = c.own;
+  size_t n = e - b;
+  if (!c.begin(st)) return false;
+  if (!c.upload_staged(c.in0, msgs + 32 * b, 32 * n, st) ||
+      !c.upload_staged(c.in1, sigs + b, n * sizeof(g2a), st) ||
+      !c.upload_staged(c.in3, rands + b, n * 8, st))
+    return false;
+  const g1a *pks = nullptr;
+  const int32_t *pre = nullptr;
+  if (!upload_pks(c, d, src, b, e, st, &pks, &pre)) return false;
+  if (verdicts) {
+    if (!c.ensure(c.out1, nseg * sizeof(int32_t))) return false;
+    if (!pipeline_verdicts(c, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), pks,
+                           c.in3.as<uint64_t>(), pre, n, seg, nseg, c.out1.as<int32_t>(), st))
+      return false;
+    HIPCHK(hipMemcpyAsync(verdicts, c.out1.p, nseg * 4, hipMemcpyDeviceToHost, st));
+  } else {
+    if (!c.ensure(c.part, sizeof(fp12)) || !c.ensure(c.err, 16)) return false;
+    if (!pipeline_partials(c, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), pks,
+                           c.in3.as<uint64_t>(), pre, n, seg, 1, 0, c.part.as<fp12>(),
+                           c.err.as<int32_t>(), st))
+      return false;
+    HIPCHK(hipMemcpyAsync(part_host, c.part.p, sizeof(fp12), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(err_host, c.err.p, 4, hipMemcpyDeviceToHost, st));
+  }
+  return true;
+}
+
+// Host-pointer batch verification over every engine device.
+bool verify_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
+                 const uint64_t *rands, size_t n, const uint32_t *seg_off, size_t nseg,
+                 int32_t *verdicts) {
+  std::shared_lock<std::shared_mutex> rl(g.reg_mu);
+  const size_t ndev = g.devs.size();
+  // ---- one large batch: per-device Miller partials, one final exponentiation
+  if (nseg == 1 && ndev > 1 && n >= 2 * kShardMinSets) {
+    size_t k = std::min(ndev, n / kShardMinSets);
+    std::vector<std::unique_ptr<Lease>> leases;
+    std::vector<fp12> parts(k);
+    std::vector<int32_t> errs(k, 1);
+    bool ok = true;
+    for (size_t j = 0; j < k && ok; j++) {
+      size_t b = n * j / k, e = n * (j + 1) / k;
+      Device &d = *g.devs[j];
+      leases.emplace_back(new Lease(d));
+      Lease &L = *leases.back();
+      uint32_t seg[2] = {0, (uint32_t)(e - b)};
+      ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, src, rands, b, e, seg, 1, nullptr,
+                                        &parts[j], &errs[j]);
+    }
+    for (auto &L : leases)
+      if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
+    leases.clear();
+    if (!ok) return false;
+    Device &d0 = *g.devs[0];
+    Lease L(d0);
+    if (!L.ok() || !L->begin(L->own)) return false;
+    hipStream_t st = L->own;
+    if (!L->upload_staged(L->in0, parts.data(), k * sizeof(fp12), st) ||
+        !L->upload_staged(L->in1, errs.data(), k * 4, st) || !L->ensure(L->out1, 16))
+      return false;
+    if (!pipeline_final(L->in0.as<fp12>(), L->in1.as<int32_t>(), k, 1, L->out1.as<int32_t>(), st))
+      return false;
+    HIPCHK(hipMemcpyAsync(verdicts, L->out1.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return true;
+  }
+  // ---- whole segments per device, contiguous groups balanced by set count
+  size_t k = 1;
+  if (ndev > 1 && nseg > 1) k = std::min({ndev, nseg, std::max<size_t>(1, n / kShardMinSets)});
+  std::vector<size_t> cut(k + 1, 0);  // segment boundaries of the groups
+  cut[k] = nseg;
+  for (size_t j = 1; j < k; j++) {
+    size_t target = n * j / k, s = cut[j - 1];
+    while (s < nseg && seg_off[s] < target) s++;
+    cut[j] = std::max(s, cut[j - 1]);
+  }
+  std::vector<std::unique_ptr<Lease>> leases;
+  std::vector<std::vector<uint32_t>> segs(k);
+  bool ok = true;
+  for (size_t j = 0; j < k && ok; j++) {
+    size_t s0 = cut[j], s1 = cut[j + 1];
+    if (s1 == s0) continue;
+    size_t b = seg_off[s0], e = seg_off[s1];
+    segs[j].resize(s1 - s0 + 1);
+    for (size_t s = s0; s <= s1; s++) segs[j][s - s0] = seg_off[s] - (uint32_t)b;
+    Device &d = k == 1 ? pick_device() : *g.devs[j];
+    leases.emplace_back(new Lease(d));
+    Lease &L = *leases.back();
+    ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, src, rands, b, e, segs[j].data(),
+                                      s1 - s0, verdicts + s0, nullptr, nullptr);
+  }
+  for (auto &L : leases)
+    if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
+  return ok;
+}
+
+void fill(int32_t *v, size_t n, int32_t x) {
+  for (size_t i = 0; i < n; i++) v[i] = x;
+}
+
+// Per-set verdicts of a batch by GPU bisection (f2): verify the batch; split every
+// failing range into up to kFan pieces and verify all pieces of a round as segments of
+// ONE submission, until the failing pieces are single sets.
+constexpr size_t kFan = 16;
+bool bisect_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
+                 const uint64_t *rands, size_t n, int32_t *set_verdicts) {
+  struct Range {
+    size_t b, e;
+  };
+  std::vector<Range> frontier{{0, n}};
+  std::vector<uint8_t> gm;
+  std::vector<g2a> gs;
+  std::vector<g1a> gp;
+  std::vector<uint32_t> gi, go;
+  std::vector<uint64_t> gr;
+  bool first = true;
+  while (!frontier.empty()) {
+    std::vector<Range> pieces;
+    for (const Range &r : frontier) {
+      size_t len = r.e - r.b;
+      size_t parts = first ? 1 : std::min(kFan, len);
+      for (size_t j = 0; j < parts; j++)
+        pieces.push_back({r.b + len * j / parts, r.b + len * (j + 1) / parts});
+    }
+    first = false;
+    // gather the pieces into one contiguous batch
+    gm.clear(); gs.clear(); gp.clear(); gi.clear(); go.clear(); gr.clear();
+    std::vector<uint32_t> seg{0};
+    if (src.off) go.push_back(0);
+    for (const Range &p : pieces) {
+      for (size_t i = p.b; i < p.e; i++) {
+        gm.insert(gm.end(), msgs + 32 * i, msgs + 32 * i + 32);
+        gs.push_back(sigs[i]);
+        gr.push_back(rands[i]);
+        if (src.pts) gp.push_back(src.pts[i]);
+        else if (src.off) {
+          gi.insert(gi.end(), src.idx + src.off[i], src.idx + src.off[i + 1]);
+          go.push_back((uint32_t)gi.size());
+        } else gi.push_back(src.idx[i]);
+      }
+      seg.push_back((uint32_t)gs.size());
+    }
+    PkSource s2;
+    if (src.pts) s2.pts = gp.data();
+    else {
+      s2.idx = gi.data();
+      if (src.off) s2.off = go.data();
+    }
+    std::vector<int32_t> v(pieces.size(), FAILED);
+    if (!verify_host(gm.data(), gs.data(), s2, gr.data(), gs.size(), seg.data(), pieces.size(),
+                     v.data()))
+      return false;
+    frontier.clear();
+    for (size_t j = 0; j < pieces.size(); j++) {
+      const Range &p = pieces[j];
+      if (v[j] == GBLS_SUCCESS)
+        fill(set_verdicts + p.b, p.e - p.b, GBLS_SUCCESS);
+      else if (p.e - p.b == 1)
+        set_verdicts[p.b] = GBLS_VERIFY_FAIL;
+      else
+        frontier.push_back(p);
+    }
+  }
+  return true;
 }
 
 }  // namespace
 
-#define API_LOCK                             \
-  std::lock_guard<std::mutex> lock__(g.mu);  \
-  t_last_error = GBLS_ERR_NONE;              \
-  if (!ensure_ready()) return -1;
+#define API_BEGIN                   \
+  t_last_error = GBLS_ERR_NONE;     \
+  if (!ensure_ready()) return FAILED;
 
 extern "C" {
 
 int gbls_init(uint32_t device_mask, uint32_t flags) {
-  (void)flags;
-  std::lock_guard<std::mutex> lock(g.mu);
   t_last_error = GBLS_ERR_NONE;
-  return engine_init_locked(device_mask) ? GBLS_SUCCESS : -1;
+  return engine_init(device_mask, flags) ? GBLS_SUCCESS : FAILED;
 }
 
 int gbls_last_error(void) { return t_last_error; }
-const char *gbls_version(void) { return "grandine-bls-mi355x 0.2 (gfx950)"; }
+const char *gbls_version(void) { return "grandine-bls-mi355x 0.3 (gfx950)"; }
+int gbls_device_count(void) { return g.ready.load() ? (int)g.devs.size() : 0; }
 
 int gbls_g1_decompress(const uint8_t (*in)[48], size_t n, int validate, gbls_p1_affine *out,
                        int32_t *status) {
-  API_LOCK
+  fill(status, n, GBLS_BAD_ENCODING);
+  API_BEGIN
   if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, &in[0][0], 48 * n) || !g.out0.ensure(n * sizeof(g1a)) ||
-      !g.out1.ensure(n * sizeof(int32_t)))
-    return -1;
-  launch_g1_decompress(g.stream, g.in0.as<uint8_t>(), (uint32_t)n, validate, g.out0.as<g1a>(),
-                       g.out1.as<int32_t>());
-  if (!download(reinterpret_cast<g1a *>(out), g.out0, n) || !download(status, g.out1, n) || !sync())
-    return -1;
+  Lease L(pick_device());
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &in[0][0], 48 * n, st) ||
+      !c.ensure(c.out0, n * sizeof(g1a)) || !c.ensure(c.out1, n * sizeof(int32_t)))
+    return FAILED;
+  launch_g1_decompress(st, c.in0.as<uint8_t>(), (uint32_t)n, validate, c.out0.as<g1a>(),
+                       c.out1.as<int32_t>());
+  if (hipMemcpyAsync(out, c.out0.p, n * sizeof(g1a), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(status, c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    fill(status, n, GBLS_BAD_ENCODING);
+    return fail(GBLS_ERR_HIP), FAILED;
+  }
   return GBLS_SUCCESS;
 }
 
 int gbls_g2_decompress(const uint8_t (*in)[96], size_t n, gbls_p2_affine *out, int32_t *status) {
-  API_LOCK
+  fill(status, n, GBLS_BAD_ENCODING);
+  API_BEGIN
   if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, &in[0][0], 96 * n) || !g.out0.ensure(n * sizeof(g2a)) ||
-      !g.out1.ensure(n * sizeof(int32_t)))
-    return -1;
-  launch_g2_decompress(g.stream, g.in0.as<uint8_t>(), (uint32_t)n, g.out0.as<g2a>(),
-                       g.out1.as<int32_t>());
-  if (!download(reinterpret_cast<g2a *>(out), g.out0, n) || !download(status, g.out1, n) || !sync())
-    return -1;
+  Lease L(pick_device());
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &in[0][0], 96 * n, st) ||
+      !c.ensure(c.out0, n * sizeof(g2a)) || !c.ensure(c.out1, n * sizeof(int32_t)))
+    return FAILED;
+  launch_g2_decompress(st, c.in0.as<uint8_t>(), (uint32_t)n, c.out0.as<g2a>(),
+                       c.out1.as<int32_t>());
+  if (hipMemcpyAsync(out, c.out0.p, n * sizeof(g2a), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(status, c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    fill(status, n, GBLS_BAD_ENCODING);
+    return fail(GBLS_ERR_HIP), FAILED;
+  }
   return GBLS_SUCCESS;
 }
 
 int gbls_g2_validate(const gbls_p2_affine *in, size_t n, int32_t *status) {
-  API_LOCK
+  fill(status, n, GBLS_POINT_NOT_IN_GROUP);
+  API_BEGIN
   if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, reinterpret_cast<const g2a *>(in), n) || !g.out1.ensure(n * sizeof(int32_t)))
-    return -1;
-  launch_g2_check(g.stream, g.in0.as<g2a>(), (uint32_t)n, g.out1.as<int32_t>(), 0);
-  if (!download(status, g.out1, n) || !sync()) return -1;
+  Lease L(pick_device());
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, in, n * sizeof(g2a), st) ||
+      !c.ensure(c.out1, n * sizeof(int32_t)))
+    return FAILED;
+  launch_g2_check(st, c.in0.as<g2a>(), (uint32_t)n, c.out1.as<int32_t>(), 0);
+  if (hipMemcpyAsync(status, c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    fill(status, n, GBLS_POINT_NOT_IN_GROUP);
+    return fail(GBLS_ERR_HIP), FAILED;
+  }
   return GBLS_SUCCESS;
 }
 
+static int compress_impl(const void *in, size_t n, size_t in_sz, size_t out_sz, uint8_t *out,
+                         int which) {
+  API_BEGIN
+  if (n == 0) return GBLS_SUCCESS;
+  Lease L(pick_device());
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, in, n * in_sz, st) ||
+      !c.ensure(c.out0, n * out_sz))
+    return FAILED;
+  if (which == 1)
+    launch_g1_compress(st, c.in0.as<g1a>(), (uint32_t)n, c.out0.as<uint8_t>());
+  else
+    launch_g2_compress(st, c.in0.as<g2a>(), (uint32_t)n, c.out0.as<uint8_t>());
+  if (hipMemcpyAsync(out, c.out0.p, n * out_sz, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(GBLS_ERR_HIP), FAILED;
+  return GBLS_SUCCESS;
+}
 int gbls_g1_compress(const gbls_p1_affine *in, size_t n, uint8_t (*out)[48]) {
-  API_LOCK
-  if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, reinterpret_cast<const g1a *>(in), n) || !g.out0.ensure(48 * n)) return -1;
-  launch_g1_compress(g.stream, g.in0.as<g1a>(), (uint32_t)n, g.out0.as<uint8_t>());
-  if (!download(&out[0][0], g.out0, 48 * n) || !sync()) return -1;
-  return GBLS_SUCCESS;
+  return compress_impl(in, n, sizeof(g1a), 48, &out[0][0], 1);
+}
+int gbls_g2_compress(const gbls_p2_affine *in, size_t n, uint8_t (*out)[96]) {
+  return compress_impl(in, n, sizeof(g2a), 96, &out[0][0], 2);
 }
 
-int gbls_g2_compress(const gbls_p2_affine *in, size_t n, uint8_t (*out)[96]) {
-  API_LOCK
-  if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, reinterpret_cast<const g2a *>(in), n) || !g.out0.ensure(96 * n)) return -1;
-  launch_g2_compress(g.stream, g.in0.as<g2a>(), (uint32_t)n, g.out0.as<uint8_t>());
-  if (!download(&out[0][0], g.out0, 96 * n) || !sync()) return -1;
+// segmented aggregation of points (which = 1: G1, 2: G2) or of registry keys (which = 3)
+static int aggregate_impl(const void *pts, const uint32_t *idx, const uint32_t *seg_offsets,
+                          size_t nseg, void *out, int32_t *status, int which) {
+  fill(status, nseg, GBLS_AGGR_TYPE_MISMATCH);
+  API_BEGIN
+  if (nseg == 0) return GBLS_SUCCESS;
+  if (!seg_offsets || seg_offsets[0] != 0) return fail(GBLS_ERR_ARG), FAILED;
+  for (size_t s = 0; s < nseg; s++)
+    if (seg_offsets[s + 1] < seg_offsets[s]) return fail(GBLS_ERR_ARG), FAILED;
+  size_t n = seg_offsets[nseg];
+  size_t psz = which == 2 ? sizeof(g2a) : sizeof(g1a);
+  std::shared_lock<std::shared_mutex> rl(g.reg_mu);
+  Device &d = pick_device();
+  Lease L(d);
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) ||
+      !c.upload_staged(c.in0, which == 3 ? (const void *)idx : pts, n * (which == 3 ? 4 : psz), st) ||
+      !c.upload_staged(c.in1, seg_offsets, (nseg + 1) * 4, st) || !c.ensure(c.out0, nseg * psz) ||
+      !c.ensure(c.out1, nseg * sizeof(int32_t)))
+    return FAILED;
+  if (which == 1)
+    launch_g1_aggregate_seg(st, c.in0.as<g1a>(), c.in1.as<uint32_t>(), (uint32_t)nseg,
+                            c.out0.as<g1a>(), c.out1.as<int32_t>());
+  else if (which == 2)
+    launch_g2_aggregate_seg(st, c.in0.as<g2a>(), c.in1.as<uint32_t>(), (uint32_t)nseg,
+                            c.out0.as<g2a>(), c.out1.as<int32_t>());
+  else
+    launch_g1_aggregate_idx(st, d.reg.as<g1a>(), (uint32_t)g.reg_n, c.in0.as<uint32_t>(),
+                            c.in1.as<uint32_t>(), (uint32_t)nseg, c.out0.as<g1a>(),
+                            c.out1.as<int32_t>());
+  if (hipMemcpyAsync(out, c.out0.p, nseg * psz, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(status, c.out1.p, nseg * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    fill(status, nseg, GBLS_AGGR_TYPE_MISMATCH);
+    return fail(GBLS_ERR_HIP), FAILED;
+  }
   return GBLS_SUCCESS;
 }
 
 int gbls_g1_aggregate_segments(const gbls_p1_affine *pks, const uint32_t *seg_offsets, size_t nseg,
                                gbls_p1_affine *out, int32_t *status) {
-  API_LOCK
-  if (nseg == 0) return GBLS_SUCCESS;
-  size_t n = seg_offsets[nseg];
-  if (!upload(g.in0, reinterpret_cast<const g1a *>(pks), n) ||
-      !upload(g.in1, seg_offsets, nseg + 1) || !g.out0.ensure(nseg * sizeof(g1a)) ||
-      !g.out1.ensure(nseg * sizeof(int32_t)))
-    return -1;
-  launch_g1_aggregate_seg(g.stream, g.in0.as<g1a>(), g.in1.as<uint32_t>(), (uint32_t)nseg,
-                          g.out0.as<g1a>(), g.out1.as<int32_t>());
-  if (!download(reinterpret_cast<g1a *>(out), g.out0, nseg) || !download(status, g.out1, nseg) ||
-      !sync())
-    return -1;
-  return GBLS_SUCCESS;
+  return aggregate_impl(pks, nullptr, seg_offsets, nseg, out, status, 1);
+}
+int gbls_g2_aggregate_segments(const gbls_p2_affine *sigs, const uint32_t *seg_offsets,
+                               size_t nseg, gbls_p2_affine *out, int32_t *status) {
+  return aggregate_impl(sigs, nullptr, seg_offsets, nseg, out, status, 2);
+}
+int gbls_g1_aggregate_indexed(const uint32_t *idx, const uint32_t *seg_offsets, size_t nseg,
+                              gbls_p1_affine *out, int32_t *status) {
+  return aggregate_impl(nullptr, idx, seg_offsets, nseg, out, status, 3);
 }
 
 int gbls_g1_aggregate(const gbls_p1_affine *pks, size_t n, gbls_p1_affine *out) {
   uint32_t off[2] = {0, (uint32_t)n};
-  int32_t st = GBLS_SUCCESS;
+  int32_t st = GBLS_AGGR_TYPE_MISMATCH;
   if (n == 0) {
     std::memset(out, 0, sizeof(*out));
     return GBLS_AGGR_TYPE_MISMATCH;
@@ -435,42 +922,76 @@ int gbls_g1_aggregate(const gbls_p1_affine *pks, size_t n, gbls_p1_affine *out) 
 }
 
 int gbls_g2_aggregate(const gbls_p2_affine *sigs, size_t n, gbls_p2_affine *out) {
-  API_LOCK
   uint32_t off[2] = {0, (uint32_t)n};
-  if (!upload(g.in0, reinterpret_cast<const g2a *>(sigs), n) || !upload(g.in1, off, 2) ||
-      !g.out0.ensure(sizeof(g2a)))
-    return -1;
-  launch_g2_aggregate_seg(g.stream, g.in0.as<g2a>(), g.in1.as<uint32_t>(), 1, g.out0.as<g2a>());
-  if (!download(reinterpret_cast<g2a *>(out), g.out0, 1) || !sync()) return -1;
+  int32_t st = GBLS_AGGR_TYPE_MISMATCH;
+  if (n == 0) {
+    std::memset(out, 0, sizeof(*out));
+    return GBLS_AGGR_TYPE_MISMATCH;
+  }
+  int rc = gbls_g2_aggregate_segments(sigs, off, 1, out, &st);
+  return rc != GBLS_SUCCESS ? rc : st;
+}
+
+// m independent checks e(pk_i, H(m_i)) == e(g1, sig_i), each its own segment (r_i = 1),
+// with the signature subgroup check (and, for FAV, the key aggregation status) folded
+// into the pre-flags.  mode 0: one key per check (pts); 1: aggregate pts per check
+// (seg_off); 2: aggregate registry keys idx per check (seg_off).
+static int single_checks(const g2a *sigs, const uint8_t *msg_data, const uint32_t *msg_off,
+                         const void *keys, const uint32_t *seg_off, size_t m, int mode,
+                         int32_t *verdicts) {
+  fill(verdicts, m, GBLS_VERIFY_FAIL);
+  API_BEGIN
+  if (m == 0) return GBLS_SUCCESS;
+  if (mode && !valid_offsets(seg_off, m, seg_off ? seg_off[m] : 0))
+    return fail(GBLS_ERR_ARG), FAILED;
+  size_t nkeys = mode ? seg_off[m] : m;
+  std::shared_lock<std::shared_mutex> rl(g.reg_mu);
+  Device &d = pick_device();
+  Lease L(d);
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  std::vector<uint32_t> ident(m + 1);
+  for (size_t i = 0; i <= m; i++) ident[i] = (uint32_t)i;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, sigs, m * sizeof(g2a), st) ||
+      !c.upload_staged(c.in1, msg_data, msg_off[m] ? msg_off[m] : 1, st) ||
+      !c.upload_staged(c.in2, msg_off, (m + 1) * 4, st) ||
+      !c.upload_staged(c.in4, keys, nkeys * (mode == 2 ? 4 : sizeof(g1a)), st) ||
+      !c.ensure(c.in3, m * sizeof(g1a)) || !c.ensure(c.out0, m * sizeof(int32_t)) ||
+      !c.ensure(c.out1, m * sizeof(int32_t)))
+    return FAILED;
+  const g1a *pks;
+  if (mode == 0) {
+    pks = c.in4.as<g1a>();
+    if (hipMemsetAsync(c.out0.p, 0, m * 4, st) != hipSuccess) return fail(GBLS_ERR_HIP), FAILED;
+  } else {
+    if (!c.upload_staged(c.in5, seg_off, (m + 1) * 4, st)) return FAILED;
+    if (mode == 1)
+      launch_g1_aggregate_seg(st, c.in4.as<g1a>(), c.in5.as<uint32_t>(), (uint32_t)m,
+                              c.in3.as<g1a>(), c.out0.as<int32_t>());
+    else
+      launch_g1_aggregate_idx(st, d.reg.as<g1a>(), (uint32_t)g.reg_n, c.in4.as<uint32_t>(),
+                              c.in5.as<uint32_t>(), (uint32_t)m, c.in3.as<g1a>(),
+                              c.out0.as<int32_t>());
+    pks = c.in3.as<g1a>();
+  }
+  launch_g2_check(st, c.in0.as<g2a>(), (uint32_t)m, c.out0.as<int32_t>(), 1);
+  if (!pipeline_verdicts(c, c.in1.as<uint8_t>(), c.in2.as<uint32_t>(), c.in0.as<g2a>(), pks,
+                         nullptr, c.out0.as<int32_t>(), m, ident.data(), m, c.out1.as<int32_t>(),
+                         st))
+    return FAILED;
+  if (hipMemcpyAsync(verdicts, c.out1.p, m * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    fill(verdicts, m, GBLS_VERIFY_FAIL);
+    return fail(GBLS_ERR_HIP), FAILED;
+  }
   return GBLS_SUCCESS;
 }
 
-// m independent checks e(pk_i, H(m_i)) == e(g1, sig_i), each its own segment
-// (r_i = 1), with the signature subgroup check folded into the pre-flags.
 int gbls_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                 const uint32_t *msg_off, const gbls_p1_affine *pks, size_t m,
                                 int32_t *verdicts) {
-  API_LOCK
-  if (m == 0) return GBLS_SUCCESS;
-  for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
-  std::vector<uint32_t> ident = identity_offsets(m);
-  if (!upload(g.in0, reinterpret_cast<const g2a *>(sigs), m) ||
-      !upload(g.in1, msg_data, msg_off[m] ? msg_off[m] : 1) || !upload(g.in2, msg_off, m + 1) ||
-      !upload(g.in3, reinterpret_cast<const g1a *>(pks), m) || !g.in5.ensure(m * sizeof(int32_t)) ||
-      !g.out1.ensure(m * sizeof(int32_t)))
-    return -1;
-  if (hipMemsetAsync(g.in5.p, 0, m * sizeof(int32_t), g.stream) != hipSuccess)
-    return (t_last_error = GBLS_ERR_HIP), -1;
-  launch_g2_check(g.stream, g.in0.as<g2a>(), (uint32_t)m, g.in5.as<int32_t>(), 1);
-  if (!pipeline_verdicts(g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), g.in0.as<g2a>(), g.in3.as<g1a>(),
-                         nullptr, g.in5.as<int32_t>(), m, ident.data(), m, g.out1.as<int32_t>(),
-                         g.stream))
-    return -1;
-  if (!download(verdicts, g.out1, m) || !sync()) {
-    for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
-    return -1;
-  }
-  return GBLS_SUCCESS;
+  return single_checks(reinterpret_cast<const g2a *>(sigs), msg_data, msg_off, pks, nullptr, m, 0,
+                       verdicts);
 }
 
 int gbls_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
@@ -486,30 +1007,15 @@ int gbls_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
 int gbls_fast_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                      const uint32_t *msg_off, const gbls_p1_affine *pks,
                                      const uint32_t *seg_off, size_t m, int32_t *verdicts) {
-  API_LOCK
-  if (m == 0) return GBLS_SUCCESS;
-  for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
-  size_t npk = seg_off[m];
-  std::vector<uint32_t> ident = identity_offsets(m);
-  if (!upload(g.in0, reinterpret_cast<const g2a *>(sigs), m) ||
-      !upload(g.in1, msg_data, msg_off[m] ? msg_off[m] : 1) || !upload(g.in2, msg_off, m + 1) ||
-      !upload(g.in4, reinterpret_cast<const g1a *>(pks), npk ? npk : 1) ||
-      !upload(g.in5, seg_off, m + 1) || !g.in3.ensure(m * sizeof(g1a)) ||
-      !g.out0.ensure(m * sizeof(int32_t)) || !g.out1.ensure(m * sizeof(int32_t)))
-    return -1;
-  // aggregate pks per message (status AGGR_TYPE_MISMATCH for empty -> pre-flag)
-  launch_g1_aggregate_seg(g.stream, g.in4.as<g1a>(), g.in5.as<uint32_t>(), (uint32_t)m,
-                          g.in3.as<g1a>(), g.out0.as<int32_t>());
-  launch_g2_check(g.stream, g.in0.as<g2a>(), (uint32_t)m, g.out0.as<int32_t>(), 1);
-  if (!pipeline_verdicts(g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), g.in0.as<g2a>(), g.in3.as<g1a>(),
-                         nullptr, g.out0.as<int32_t>(), m, ident.data(), m, g.out1.as<int32_t>(),
-                         g.stream))
-    return -1;
-  if (!download(verdicts, g.out1, m) || !sync()) {
-    for (size_t i = 0; i < m; i++) verdicts[i] = GBLS_VERIFY_FAIL;
-    return -1;
-  }
-  return GBLS_SUCCESS;
+  return single_checks(reinterpret_cast<const g2a *>(sigs), msg_data, msg_off, pks, seg_off, m, 1,
+                       verdicts);
+}
+
+int gbls_fast_aggregate_verify_indexed(const gbls_p2_affine *sigs, const uint8_t *msg_data,
+                                       const uint32_t *msg_off, const uint32_t *pk_idx,
+                                       const uint32_t *seg_off, size_t m, int32_t *verdicts) {
+  return single_checks(reinterpret_cast<const g2a *>(sigs), msg_data, msg_off, pk_idx, seg_off,
+                       m, 2, verdicts);
 }
 
 int gbls_fast_aggregate_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
@@ -528,21 +1034,16 @@ int gbls_fast_aggregate_verify(const gbls_p2_affine *sig, const uint8_t *msg, si
 int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
                                const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                const uint32_t *seg_off, size_t nseg, int32_t *verdicts) {
-  API_LOCK
-  for (size_t s = 0; s < nseg; s++) verdicts[s] = GBLS_VERIFY_FAIL;
+  fill(verdicts, nseg, GBLS_VERIFY_FAIL);
+  API_BEGIN
   if (nseg == 0) return GBLS_SUCCESS;
-  if (seg_off[nseg] != n) return (t_last_error = GBLS_ERR_ARG), -1;
-  if (!upload(g.in0, &msgs[0][0], 32 * n) || !upload(g.in1, reinterpret_cast<const g2a *>(sigs), n) ||
-      !upload(g.in2, reinterpret_cast<const g1a *>(pks), n) || !upload(g.in3, rands, n) ||
-      !g.out1.ensure(nseg * sizeof(int32_t)))
-    return -1;
-  if (!pipeline_verdicts(g.in0.as<uint8_t>(), nullptr, g.in1.as<g2a>(), g.in2.as<g1a>(),
-                         g.in3.as<uint64_t>(), nullptr, n, seg_off, nseg, g.out1.as<int32_t>(),
-                         g.stream))
-    return -1;
-  if (!download(verdicts, g.out1, nseg) || !sync()) {
-    for (size_t s = 0; s < nseg; s++) verdicts[s] = GBLS_VERIFY_FAIL;
-    return -1;
+  if (!valid_offsets(seg_off, nseg, n)) return fail(GBLS_ERR_ARG), FAILED;
+  PkSource src;
+  src.pts = reinterpret_cast<const g1a *>(pks);
+  if (!verify_host(&msgs[0][0], reinterpret_cast<const g2a *>(sigs), src, rands, n, seg_off, nseg,
+                   verdicts)) {
+    fill(verdicts, nseg, GBLS_VERIFY_FAIL);
+    return FAILED;
   }
   return GBLS_SUCCESS;
 }
@@ -559,106 +1060,291 @@ int gbls_multi_verify(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
   return v;
 }
 
+int gbls_multi_verify_indexed(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
+                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                              const uint64_t *rands, size_t n) {
+  API_BEGIN
+  if (n == 0) return GBLS_VERIFY_FAIL;
+  if (pk_off && !valid_offsets(pk_off, n, pk_off[n])) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
+  PkSource src;
+  src.idx = pk_idx;
+  src.off = pk_off;
+  uint32_t off[2] = {0, (uint32_t)n};
+  int32_t v = GBLS_VERIFY_FAIL;
+  if (!verify_host(&msgs[0][0], reinterpret_cast<const g2a *>(sigs), src, rands, n, off, 1, &v))
+    return GBLS_VERIFY_FAIL;
+  return v;
+}
+
+int gbls_multi_verify_bisect(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
+                             const gbls_p1_affine *pks, const uint32_t *pk_idx,
+                             const uint32_t *pk_off, const uint64_t *rands, size_t n,
+                             int32_t *set_verdicts) {
+  fill(set_verdicts, n, GBLS_VERIFY_FAIL);
+  API_BEGIN
+  if (n == 0) return GBLS_SUCCESS;
+  if (pk_off && !valid_offsets(pk_off, n, pk_off[n])) return fail(GBLS_ERR_ARG), FAILED;
+  PkSource src;
+  src.pts = reinterpret_cast<const g1a *>(pks);
+  src.idx = pks ? nullptr : pk_idx;
+  src.off = pks ? nullptr : pk_off;
+  if (!src.pts && !src.idx) return fail(GBLS_ERR_ARG), FAILED;
+  if (!bisect_host(&msgs[0][0], reinterpret_cast<const g2a *>(sigs), src, rands, n,
+                   set_verdicts)) {
+    fill(set_verdicts, n, GBLS_VERIFY_FAIL);
+    return FAILED;
+  }
+  return GBLS_SUCCESS;
+}
+
+// ---- device-pointer variants (inputs resident in HBM, asynchronous on the caller's stream)
+static int device_verify(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
+                         const uint64_t *rands, size_t n, const uint32_t *seg_off, size_t nseg,
+                         int32_t *verdicts, fp12 *partials, int32_t *seg_err, void *stream) {
+  API_BEGIN
+  if (nseg == 0) return GBLS_SUCCESS;
+  if (!valid_offsets(seg_off, nseg, n)) return fail(GBLS_ERR_ARG), FAILED;
+  Device *d = current_device();
+  if (!d) return fail(GBLS_ERR_ARG), FAILED;
+  std::shared_lock<std::shared_mutex> rl(g.reg_mu);
+  Lease L(*d, true, (hipStream_t)stream);
+  Ctx &c = *L;
+  hipStream_t st = (hipStream_t)stream;
+  if (!L.ok() || !c.begin(st)) return FAILED;
+  const g1a *pks = nullptr;
+  const int32_t *pre = nullptr;
+  if (!resolve_pks(c, *d, src, n, st, &pks, &pre)) return FAILED;
+  bool ok = verdicts ? pipeline_verdicts(c, msgs, nullptr, sigs, pks, rands, pre, n, seg_off, nseg,
+                                         verdicts, st)
+                     : pipeline_partials(c, msgs, nullptr, sigs, pks, rands, pre, n, seg_off,
+                                         nseg, 0, partials, seg_err, st);
+  return ok ? GBLS_SUCCESS : FAILED;
+}
+
 int gbls_multi_verify_segments_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
                                       const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                       const uint32_t *seg_off, size_t nseg, int32_t *verdicts,
                                       void *stream) {
-  API_LOCK
-  if (nseg == 0) return GBLS_SUCCESS;
-  if (seg_off[nseg] != n) return (t_last_error = GBLS_ERR_ARG), -1;
-  hipStream_t st = stream ? (hipStream_t)stream : g.stream;
-  return pipeline_verdicts(msgs, nullptr, reinterpret_cast<const g2a *>(sigs),
-                           reinterpret_cast<const g1a *>(pks), rands, nullptr, n, seg_off, nseg,
-                           verdicts, st)
-             ? GBLS_SUCCESS
-             : -1;
+  PkSource src;
+  src.pts = reinterpret_cast<const g1a *>(pks);
+  return device_verify(msgs, reinterpret_cast<const g2a *>(sigs), src, rands, n, seg_off, nseg,
+                       verdicts, nullptr, nullptr, stream);
+}
+
+int gbls_multi_verify_indexed_segments_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
+                                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                                              const uint64_t *rands, size_t n,
+                                              const uint32_t *seg_off, size_t nseg,
+                                              int32_t *verdicts, void *stream) {
+  PkSource src;
+  src.idx = pk_idx;
+  src.off = pk_off;
+  return device_verify(msgs, reinterpret_cast<const g2a *>(sigs), src, rands, n, seg_off, nseg,
+                       verdicts, nullptr, nullptr, stream);
 }
 
 int gbls_multi_verify_partials_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
                                       const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                       const uint32_t *seg_off, size_t nseg, gbls_fp12 *partials,
                                       int32_t *seg_err, void *stream) {
-  API_LOCK
-  if (nseg == 0) return GBLS_SUCCESS;
-  if (seg_off[nseg] != n) return (t_last_error = GBLS_ERR_ARG), -1;
-  hipStream_t st = stream ? (hipStream_t)stream : g.stream;
-  return pipeline_partials(msgs, nullptr, reinterpret_cast<const g2a *>(sigs),
-                           reinterpret_cast<const g1a *>(pks), rands, nullptr, n, seg_off, nseg,
-                           reinterpret_cast<fp12 *>(partials), seg_err, st)
-             ? GBLS_SUCCESS
-             : -1;
+  PkSource src;
+  src.pts = reinterpret_cast<const g1a *>(pks);
+  return device_verify(msgs, reinterpret_cast<const g2a *>(sigs), src, rands, n, seg_off, nseg,
+                       nullptr, reinterpret_cast<fp12 *>(partials), seg_err, stream);
+}
+
+int gbls_multi_verify_indexed_partials_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
+                                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                                              const uint64_t *rands, size_t n,
+                                              const uint32_t *seg_off, size_t nseg,
+                                              gbls_fp12 *partials, int32_t *seg_err,
+                                              void *stream) {
+  PkSource src;
+  src.idx = pk_idx;
+  src.off = pk_off;
+  return device_verify(msgs, reinterpret_cast<const g2a *>(sigs), src, rands, n, seg_off, nseg,
+                       nullptr, reinterpret_cast<fp12 *>(partials), seg_err, stream);
 }
 
 int gbls_final_verify_partials_device(const gbls_fp12 *partials, const int32_t *seg_err,
                                       size_t nparts, size_t nseg, int32_t *verdicts, void *stream) {
-  API_LOCK
+  API_BEGIN
   if (nseg == 0) return GBLS_SUCCESS;
-  hipStream_t st = stream ? (hipStream_t)stream : g.stream;
+  if (nparts == 0) return fail(GBLS_ERR_ARG), FAILED;
+  Device *d = current_device();
+  if (!d) return fail(GBLS_ERR_ARG), FAILED;
+  Lease L(*d, true, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  if (!L.ok() || !L->begin(st)) return FAILED;
   return pipeline_final(reinterpret_cast<const fp12 *>(partials), seg_err, nparts, nseg, verdicts,
                         st)
              ? GBLS_SUCCESS
-             : -1;
+             : FAILED;
 }
 
-int gbls_sk_to_pk(const uint8_t (*sks)[32], size_t n, gbls_p1_affine *out) {
-  API_LOCK
-  if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, &sks[0][0], 32 * n) || !g.out0.ensure(n * sizeof(g1a))) return -1;
-  launch_sk_to_pk(g.stream, g.in0.as<uint8_t>(), (uint32_t)n, g.out0.as<g1a>());
-  if (!download(reinterpret_cast<g1a *>(out), g.out0, n) || !sync()) return -1;
+// C3 on device-resident inputs: m sync-committee checks, 32-byte messages, keys from the
+// registry (pk_idx / pk_off device arrays, pk_off[0] == 0 and non-decreasing)
+int gbls_fast_aggregate_verify_indexed_device(const gbls_p2_affine *sigs, const uint8_t *msgs,
+                                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                                              size_t m, int32_t *verdicts, void *stream) {
+  API_BEGIN
+  if (m == 0) return GBLS_SUCCESS;
+  Device *d = current_device();
+  if (!d) return fail(GBLS_ERR_ARG), FAILED;
+  std::shared_lock<std::shared_mutex> rl(g.reg_mu);
+  Lease L(*d, true, (hipStream_t)stream);
+  Ctx &c = *L;
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<uint32_t> ident(m + 1);
+  for (size_t i = 0; i <= m; i++) ident[i] = (uint32_t)i;
+  if (!L.ok() || !c.begin(st) || !c.ensure(c.in3, m * sizeof(g1a)) ||
+      !c.ensure(c.out0, m * sizeof(int32_t)))
+    return FAILED;
+  {
+    StageTimer t(S_PK_GATHER, st);
+    launch_g1_aggregate_idx(st, d->reg.as<g1a>(), (uint32_t)g.reg_n, pk_idx, pk_off, (uint32_t)m,
+                            c.in3.as<g1a>(), c.out0.as<int32_t>());
+  }
+  const g2a *sg = reinterpret_cast<const g2a *>(sigs);
+  launch_g2_check(st, sg, (uint32_t)m, c.out0.as<int32_t>(), 1);
+  return pipeline_verdicts(c, msgs, nullptr, sg, c.in3.as<g1a>(), nullptr, c.out0.as<int32_t>(), m,
+                           ident.data(), m, verdicts, st)
+             ? GBLS_SUCCESS
+             : FAILED;
+}
+
+// ---- validator registry (f1): bulk decompress + validate on the device, replicated
+int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t *status) {
+  fill(status, n, GBLS_BAD_ENCODING);
+  API_BEGIN
+  std::unique_lock<std::shared_mutex> wl(g.reg_mu);
+  size_t new_n = std::max(g.reg_n, first + n);
+  if (new_n > 0xffffffffull) return fail(GBLS_ERR_ARG), FAILED;
+  for (size_t j = 0; j < g.devs.size(); j++) {
+    Device &d = *g.devs[j];
+    if (hipSetDevice(d.hipdev) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      return fail(GBLS_ERR_HIP), FAILED;
+    if (new_n * sizeof(g1a) > d.reg.cap) {  // grow, keeping the entries already loaded
+      Buf nb;
+      if (!nb.ensure(new_n * sizeof(g1a))) return fail(GBLS_ERR_HIP), FAILED;
+      if (hipMemset(nb.p, 0, nb.cap) != hipSuccess) return fail(GBLS_ERR_HIP), FAILED;
+      if (g.reg_n && hipMemcpy(nb.p, d.reg.p, g.reg_n * sizeof(g1a), hipMemcpyDeviceToDevice) !=
+                         hipSuccess)
+        return fail(GBLS_ERR_HIP), FAILED;
+      if (d.reg.p) (void)hipFree(d.reg.p);
+      d.reg = nb;
+    }
+  }
+  if (n) {
+    std::vector<int32_t> st0(n);
+    for (size_t j = 0; j < g.devs.size(); j++) {
+      Device &d = *g.devs[j];
+      Lease L(d);
+      Ctx &c = *L;
+      hipStream_t st = c.own;
+      if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &pks[0][0], 48 * n, st) ||
+          !c.ensure(c.out1, n * sizeof(int32_t)))
+        return FAILED;
+      launch_g1_decompress(st, c.in0.as<uint8_t>(), (uint32_t)n, 1, d.reg.as<g1a>() + first,
+                           c.out1.as<int32_t>());
+      if (hipMemcpyAsync(st0.data(), c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return fail(GBLS_ERR_HIP), FAILED;
+    }
+    std::memcpy(status, st0.data(), n * 4);
+  }
+  g.reg_n = new_n;
   return GBLS_SUCCESS;
 }
 
-// hash_to_G2 of n messages into g.out1 (affine), optional custom DST (device pointer)
-static bool h2c_affine_locked(const uint8_t *msg_data, const uint32_t *msg_off, size_t n,
-                              const uint8_t *dst_dev, uint32_t dst_len) {
-  if (!upload(g.in1, msg_data, msg_off[n] ? msg_off[n] : 1) || !upload(g.in2, msg_off, n + 1) ||
-      !g.U.ensure(2 * n * sizeof(fp2)) || !g.Q.ensure(2 * n * sizeof(g2j)) ||
-      !g.out1.ensure(n * sizeof(g2a)))
+size_t gbls_registry_size(void) {
+  std::shared_lock<std::shared_mutex> rl(g.reg_mu);
+  return g.reg_n;
+}
+
+int gbls_sk_to_pk(const uint8_t (*sks)[32], size_t n, gbls_p1_affine *out) {
+  API_BEGIN
+  if (n == 0) return GBLS_SUCCESS;
+  Lease L(pick_device());
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &sks[0][0], 32 * n, st) ||
+      !c.ensure(c.out0, n * sizeof(g1a)))
+    return FAILED;
+  launch_sk_to_pk(st, c.in0.as<uint8_t>(), (uint32_t)n, c.out0.as<g1a>());
+  if (hipMemcpyAsync(out, c.out0.p, n * sizeof(g1a), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(GBLS_ERR_HIP), FAILED;
+  return GBLS_SUCCESS;
+}
+
+// hash_to_G2 of n messages into c.out1 (affine), optional custom DST (device pointer)
+static bool h2c_affine(Ctx &c, const uint8_t *msg_data, const uint32_t *msg_off, size_t n,
+                       const uint8_t *dst_dev, uint32_t dst_len, hipStream_t st) {
+  if (!c.upload_staged(c.in1, msg_data, msg_off[n] ? msg_off[n] : 1, st) ||
+      !c.upload_staged(c.in2, msg_off, (n + 1) * 4, st) || !c.ensure(c.U, 2 * n * sizeof(fp2)) ||
+      !c.ensure(c.Q, 2 * n * sizeof(g2j)) || !c.ensure(c.out1, n * sizeof(g2a)))
     return false;
-  launch_h2c_field(g.stream, g.in1.as<uint8_t>(), g.in2.as<uint32_t>(), (uint32_t)n, dst_dev, dst_len,
-                   g.U.as<fp2>());
-  launch_h2c_map(g.stream, g.U.as<fp2>(), (uint32_t)(2 * n), g.Q.as<g2j>());
-  launch_h2c_clear(g.stream, g.Q.as<g2j>(), (uint32_t)n, g.out1.as<g2a>());
+  launch_h2c_field(st, c.in1.as<uint8_t>(), c.in2.as<uint32_t>(), (uint32_t)n, dst_dev, dst_len,
+                   c.U.as<fp2>());
+  launch_h2c_map(st, c.U.as<fp2>(), (uint32_t)(2 * n), c.Q.as<g2j>());
+  launch_h2c_clear(st, c.Q.as<g2j>(), (uint32_t)n, c.out1.as<g2a>());
   return hipGetLastError() == hipSuccess || fail(GBLS_ERR_HIP);
 }
 
 int gbls_sign(const uint8_t (*sks)[32], const uint8_t *msg_data, const uint32_t *msg_off, size_t n,
               gbls_p2_affine *out) {
-  API_LOCK
+  API_BEGIN
   if (n == 0) return GBLS_SUCCESS;
-  if (!upload(g.in0, &sks[0][0], 32 * n) || !g.out0.ensure(n * sizeof(g2a))) return -1;
-  if (!h2c_affine_locked(msg_data, msg_off, n, nullptr, 0)) return -1;
-  launch_sign(g.stream, g.in0.as<uint8_t>(), g.out1.as<g2a>(), (uint32_t)n, g.out0.as<g2a>());
-  if (!download(reinterpret_cast<g2a *>(out), g.out0, n) || !sync()) return -1;
+  Lease L(pick_device());
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &sks[0][0], 32 * n, st) ||
+      !c.ensure(c.out0, n * sizeof(g2a)))
+    return FAILED;
+  if (!h2c_affine(c, msg_data, msg_off, n, nullptr, 0, st)) return FAILED;
+  launch_sign(st, c.in0.as<uint8_t>(), c.out1.as<g2a>(), (uint32_t)n, c.out0.as<g2a>());
+  if (hipMemcpyAsync(out, c.out0.p, n * sizeof(g2a), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(GBLS_ERR_HIP), FAILED;
   return GBLS_SUCCESS;
 }
 
 int gbls_hash_to_g2(const uint8_t *msg_data, const uint32_t *msg_off, size_t n, const uint8_t *dst,
                     size_t dst_len, gbls_p2_affine *out) {
-  API_LOCK
+  API_BEGIN
   if (n == 0) return GBLS_SUCCESS;
-  if (dst_len > 255) return (t_last_error = GBLS_ERR_ARG), -1;
-  if (!upload(g.in3, dst, dst_len ? dst_len : 1)) return -1;
-  if (!h2c_affine_locked(msg_data, msg_off, n, g.in3.as<uint8_t>(), (uint32_t)dst_len)) return -1;
-  if (!download(reinterpret_cast<g2a *>(out), g.out1, n) || !sync()) return -1;
+  if (dst_len > 255) return fail(GBLS_ERR_ARG), FAILED;
+  Lease L(pick_device());
+  Ctx &c = *L;
+  hipStream_t st = c.own;
+  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in3, dst, dst_len ? dst_len : 1, st))
+    return FAILED;
+  if (!h2c_affine(c, msg_data, msg_off, n, c.in3.as<uint8_t>(), (uint32_t)dst_len, st))
+    return FAILED;
+  if (hipMemcpyAsync(out, c.out1.p, n * sizeof(g2a), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(GBLS_ERR_HIP), FAILED;
   return GBLS_SUCCESS;
 }
 
 double gbls_measure_mad64_peak(void) {
-  std::lock_guard<std::mutex> lock(g.mu);
   if (!ensure_ready()) return 0.0;
+  Lease L(pick_device());
+  if (!L.ok()) return 0.0;
+  hipStream_t st = L->own;
+  L->begin(st);
   Buf sink;
   if (!sink.ensure(64)) return 0.0;
   const unsigned blocks = 256 * 8, threads = 256;
   const uint32_t iters = 4096;
-  launch_mad_peak(g.stream, blocks, sink.as<uint64_t>(), 16, 1);  // warm
+  launch_mad_peak(st, blocks, sink.as<uint64_t>(), 16, 1);  // warm
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  (void)hipEventRecord(a, g.stream);
-  launch_mad_peak(g.stream, blocks, sink.as<uint64_t>(), iters, 7);
-  (void)hipEventRecord(b, g.stream);
+  (void)hipEventRecord(a, st);
+  launch_mad_peak(st, blocks, sink.as<uint64_t>(), iters, 7);
+  (void)hipEventRecord(b, st);
   (void)hipEventSynchronize(b);
   float ms = 0;
   (void)hipEventElapsedTime(&ms, a, b);
@@ -670,37 +1356,35 @@ double gbls_measure_mad64_peak(void) {
 }
 
 int gbls_profile(int enable) {
-  std::lock_guard<std::mutex> lock(g.mu);
-  int prev = g.prof ? 1 : 0;
-  g.prof = enable != 0;
-  return prev;
+  bool prev = prof.on.exchange(enable != 0);
+  return prev ? 1 : 0;
 }
 
 int gbls_profile_read(double *ms, uint32_t *calls, int max_stages) {
-  std::lock_guard<std::mutex> lock(g.mu);
-  for (auto &r : g.pending) {
+  std::lock_guard<std::mutex> lk(prof.mu);
+  for (auto &r : prof.pending) {
     float t = 0;
     if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
-      g.ms[r.stage] += t;
-      g.calls[r.stage] += 1;
+      prof.ms[r.stage] += t;
+      prof.calls[r.stage] += 1;
     }
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
   }
-  g.pending.clear();
+  prof.pending.clear();
   int n = max_stages < S_COUNT ? max_stages : S_COUNT;
   for (int i = 0; i < n; i++) {
-    if (ms) ms[i] = g.ms[i];
-    if (calls) calls[i] = g.calls[i];
+    if (ms) ms[i] = prof.ms[i];
+    if (calls) calls[i] = prof.calls[i];
   }
   return S_COUNT;
 }
 
 void gbls_profile_reset(void) {
-  std::lock_guard<std::mutex> lock(g.mu);
+  std::lock_guard<std::mutex> lk(prof.mu);
   for (int i = 0; i < S_COUNT; i++) {
-    g.ms[i] = 0;
-    g.calls[i] = 0;
+    prof.ms[i] = 0;
+    prof.calls[i] = 0;
   }
 }
 

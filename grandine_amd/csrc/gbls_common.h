@@ -26,7 +26,12 @@ void launch_g2_compress(hipStream_t st, const g2a *in, uint32_t n, uint8_t *out)
 void launch_g1_aggregate_seg(hipStream_t st, const g1a *pks, const uint32_t *off, uint32_t nseg,
                              g1a *out, int32_t *status);
 void launch_g2_aggregate_seg(hipStream_t st, const g2a *pts, const uint32_t *off, uint32_t nseg,
-                             g2a *out);
+                             g2a *out, int32_t *status);
+// validator registry (f1): keys by index
+void launch_g1_aggregate_idx(hipStream_t st, const g1a *reg, uint32_t nreg, const uint32_t *idx,
+                             const uint32_t *off, uint32_t nseg, g1a *out, int32_t *status);
+void launch_g1_gather_idx(hipStream_t st, const g1a *reg, uint32_t nreg, const uint32_t *idx,
+                          uint32_t n, g1a *out, int32_t *status);
 void launch_sk_to_pk(hipStream_t st, const uint8_t *sks, uint32_t n, g1a *out);
 void launch_sign(hipStream_t st, const uint8_t *sks, const g2a *H, uint32_t n, g2a *out);
 void launch_mad_peak(hipStream_t st, unsigned blocks, uint64_t *sink, uint32_t iters, uint32_t seed);
@@ -40,11 +45,13 @@ void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H);
 // k_scalar.hip -- random-scalar products and the per-segment signature sum
 void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1a *P);
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R);
-// chunks: 4 words per level-1 workgroup {segment, half, begin, end}; seg_chunk[nseg+1]
+// chunks: 4 words per level-1 workgroup {segment, half, begin, end}; seg_chunk[nseg+1].
+// seg_err[s] = a set of s failed (infinite pk, zero scalar, pre[i] != 0) or, when
+// empty_is_error, s has no sets; an empty segment's partial is the identity otherwise.
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
-                  const g1a *pks, const int32_t *pre, g2j *part, int32_t *part_err, g1a *P, g2a *H,
-                  int32_t *seg_err);
+                  const g1a *pks, const uint64_t *rands, const int32_t *pre, int empty_is_error,
+                  g2j *part, int32_t *part_err, g1a *P, g2a *H, int32_t *seg_err);
 
 // k_lines.hip -- Miller-loop line functions of every pair
 // lines of pairs [first, first + count) of np (H indexed by pair)

@@ -67,19 +67,19 @@ __global__ void __launch_bounds__(WG) k_g2_compress(const g2a *in, uint32_t n, u
 // ---------------------------------------------------------------- launchers
 void launch_g1_decompress(hipStream_t st, const uint8_t *in, uint32_t n, int validate, g1a *out,
                           int32_t *status) {
-  k_g1_decompress<<<nblk(n), WG, 0, st>>>(in, n, validate, out, status);
+  if (n) k_g1_decompress<<<nblk(n), WG, 0, st>>>(in, n, validate, out, status);
 }
 void launch_g2_decompress(hipStream_t st, const uint8_t *in, uint32_t n, g2a *out, int32_t *status) {
-  k_g2_decompress<<<nblk(n), WG, 0, st>>>(in, n, out, status);
+  if (n) k_g2_decompress<<<nblk(n), WG, 0, st>>>(in, n, out, status);
 }
 void launch_g2_check(hipStream_t st, const g2a *in, uint32_t n, int32_t *status, int accumulate) {
-  k_g2_check<<<nblk(n), WG, 0, st>>>(in, n, status, accumulate);
+  if (n) k_g2_check<<<nblk(n), WG, 0, st>>>(in, n, status, accumulate);
 }
 void launch_g1_compress(hipStream_t st, const g1a *in, uint32_t n, uint8_t *out) {
-  k_g1_compress<<<nblk(n), WG, 0, st>>>(in, n, out);
+  if (n) k_g1_compress<<<nblk(n), WG, 0, st>>>(in, n, out);
 }
 void launch_g2_compress(hipStream_t st, const g2a *in, uint32_t n, uint8_t *out) {
-  k_g2_compress<<<nblk(n), WG, 0, st>>>(in, n, out);
+  if (n) k_g2_compress<<<nblk(n), WG, 0, st>>>(in, n, out);
 }
 
 }  // namespace gbls

@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const in
 
 void launch_final_verdict(hipStream_t st, const fp12 *partials, const int32_t *err,
                           uint32_t nparts, uint32_t nseg, int32_t *verdict) {
-  k_final_verdict<<<nseg, 64, 0, st>>>(partials, err, nparts, nseg, verdict);
+  if (nseg) k_final_verdict<<<nseg, 64, 0, st>>>(partials, err, nparts, nseg, verdict);
 }
 
 }  // namespace gbls

@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(WG) k_h2c_clear(const g2j *Q, uint32_t n, g2a 
 }
 
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
-  k_h2c_clear<<<nblk((size_t)n * 4), WG, 0, st>>>(Q, n, H);
+  if (n) k_h2c_clear<<<nblk((size_t)n * 4), WG, 0, st>>>(Q, n, H);
 }
 
 }  // namespace gbls

@@ -33,6 +33,6 @@ __global__ void __launch_bounds__(WG) k_h2c_field(const uint8_t *msg, const uint
 }
 void launch_h2c_field(hipStream_t st, const uint8_t *msg, const uint32_t *off, uint32_t n,
                       const uint8_t *dst, uint32_t dlen, fp2 *U) {
-  k_h2c_field<<<nblk(n), WG, 0, st>>>(msg, off, n, dst, dlen, U);
+  if (n) k_h2c_field<<<nblk(n), WG, 0, st>>>(msg, off, n, dst, dlen, U);
 }
 }  // namespace gbls

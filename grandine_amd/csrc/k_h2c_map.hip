@@ -14,6 +14,6 @@ __global__ void __launch_bounds__(WG) k_h2c_map(const fp2 *U, uint32_t nu, g2j *
   Q[i] = q;
 }
 void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q) {
-  k_h2c_map<<<nblk(nu), WG, 0, st>>>(U, nu, Q);
+  if (nu) k_h2c_map<<<nblk(nu), WG, 0, st>>>(U, nu, Q);
 }
 }  // namespace gbls

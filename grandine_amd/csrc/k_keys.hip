@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(WGR) k_g1_aggregate_seg(const g1a *pks, const 
 }
 
 __global__ void __launch_bounds__(WGR) k_g2_aggregate_seg(const g2a *pts, const uint32_t *off,
-                                                          uint32_t nseg, g2a *out) {
+                                                          uint32_t nseg, g2a *out, int32_t *st) {
   uint32_t s = blockIdx.x;
   if (s >= nseg) return;
   uint32_t b = off[s], e = off[s + 1];
@@ -50,7 +50,74 @@ __global__ void __launch_bounds__(WGR) k_g2_aggregate_seg(const g2a *pts, const 
     g2a r;
     jac_to_aff(r, acc);
     out[s] = r;
+    if (st) st[s] = (e > b) ? ST_SUCCESS : ST_AGGR_TYPE_MISMATCH;
   }
+}
+
+// ---------------------------------------------------------------- validator registry (f1)
+// Public keys addressed by validator index into a device-resident table of decompressed,
+// validated keys (the CachedPublicKey cache, bls/src/cached_public_key.rs:104-108, one
+// per Validator.pubkey, types/src/phase0/containers.rs:229).  Invalid or out-of-range
+// entries are all-zero (infinity), which every verification path rejects.
+
+// one workgroup per segment: sum of reg[idx[off[s] .. off[s+1])] (Triple::verify_aggregate,
+// helper_functions/src/verifier.rs:387-405); st = AGGR_TYPE_MISMATCH when empty,
+// BAD_ENCODING when an index is out of range.  An infinite sum is a SUCCESS (as in
+// AggregatePublicKey::aggregate); the verification paths reject infinite keys.
+__global__ void __launch_bounds__(WGR) k_g1_aggregate_idx(const g1a *reg, uint32_t nreg,
+                                                          const uint32_t *idx, const uint32_t *off,
+                                                          uint32_t nseg, g1a *out, int32_t *st) {
+  __shared__ int32_t oob_sh;
+  uint32_t s = blockIdx.x;
+  if (s >= nseg) return;
+  if (threadIdx.x == 0) oob_sh = 0;
+  __syncthreads();
+  uint32_t b = off[s], e = off[s + 1];
+  g1j acc;
+  jac_set_inf(acc);
+  int32_t oob = 0;
+  for (uint32_t i = b + threadIdx.x; i < e; i += WGR) {
+    uint32_t v = idx[i];
+    if (v < nreg)
+      jac_add_aff(acc, acc, reg[v]);
+    else
+      oob = 1;
+  }
+  if (oob) atomicOr(&oob_sh, 1);
+  wg_reduce_jac(acc);
+  if (threadIdx.x == 0) {
+    g1a r;
+    jac_to_aff(r, acc);
+    int32_t status = ST_SUCCESS;
+    if (e == b)
+      status = ST_AGGR_TYPE_MISMATCH;
+    else if (oob_sh)
+      status = ST_BAD_ENCODING;
+    if (status != ST_SUCCESS) {
+      fp_zero(r.x);
+      fp_zero(r.y);
+    }
+    out[s] = r;
+    st[s] = status;
+  }
+}
+
+// one key per set: out[i] = reg[idx[i]] (all-zero + BAD_ENCODING when out of range)
+__global__ void __launch_bounds__(WG) k_g1_gather_idx(const g1a *reg, uint32_t nreg,
+                                                      const uint32_t *idx, uint32_t n, g1a *out,
+                                                      int32_t *st) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  uint32_t v = idx[i];
+  g1a r;
+  if (v < nreg) {
+    r = reg[v];
+  } else {
+    fp_zero(r.x);
+    fp_zero(r.y);
+  }
+  out[i] = r;
+  st[i] = v < nreg ? ST_SUCCESS : ST_BAD_ENCODING;
 }
 
 // ---------------------------------------------------------------- key material (a15)
@@ -121,17 +188,25 @@ __global__ void __launch_bounds__(256) k_mad_peak(uint64_t *sink, uint32_t iters
 // ---------------------------------------------------------------- launchers
 void launch_g1_aggregate_seg(hipStream_t st, const g1a *pks, const uint32_t *off, uint32_t nseg,
                              g1a *out, int32_t *status) {
-  k_g1_aggregate_seg<<<nseg, WGR, 0, st>>>(pks, off, nseg, out, status);
+  if (nseg) k_g1_aggregate_seg<<<nseg, WGR, 0, st>>>(pks, off, nseg, out, status);
 }
 void launch_g2_aggregate_seg(hipStream_t st, const g2a *pts, const uint32_t *off, uint32_t nseg,
-                             g2a *out) {
-  k_g2_aggregate_seg<<<nseg, WGR, 0, st>>>(pts, off, nseg, out);
+                             g2a *out, int32_t *status) {
+  if (nseg) k_g2_aggregate_seg<<<nseg, WGR, 0, st>>>(pts, off, nseg, out, status);
+}
+void launch_g1_aggregate_idx(hipStream_t st, const g1a *reg, uint32_t nreg, const uint32_t *idx,
+                             const uint32_t *off, uint32_t nseg, g1a *out, int32_t *status) {
+  if (nseg) k_g1_aggregate_idx<<<nseg, WGR, 0, st>>>(reg, nreg, idx, off, nseg, out, status);
+}
+void launch_g1_gather_idx(hipStream_t st, const g1a *reg, uint32_t nreg, const uint32_t *idx,
+                          uint32_t n, g1a *out, int32_t *status) {
+  if (n) k_g1_gather_idx<<<nblk(n), WG, 0, st>>>(reg, nreg, idx, n, out, status);
 }
 void launch_sk_to_pk(hipStream_t st, const uint8_t *sks, uint32_t n, g1a *out) {
-  k_sk_to_pk<<<nblk(n), WG, 0, st>>>(sks, n, out);
+  if (n) k_sk_to_pk<<<nblk(n), WG, 0, st>>>(sks, n, out);
 }
 void launch_sign(hipStream_t st, const uint8_t *sks, const g2a *H, uint32_t n, g2a *out) {
-  k_sign<<<nblk(n), WG, 0, st>>>(sks, H, n, out);
+  if (n) k_sign<<<nblk(n), WG, 0, st>>>(sks, H, n, out);
 }
 void launch_mad_peak(hipStream_t st, unsigned blocks, uint64_t *sink, uint32_t iters, uint32_t seed) {
   k_mad_peak<<<blocks, 256, 0, st>>>(sink, iters, seed);

@@ -82,15 +82,15 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
 void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1a *P,
                     const uint32_t *couples, uint32_t ncouple, fp12 *V0) {
   dim3 grid(nblk(ncouple), ML_EVENTS);
-  k_ml_leaf<<<grid, WG, 0, st>>>(lines, np, P, couples, ncouple, V0);
+  if (ncouple) k_ml_leaf<<<grid, WG, 0, st>>>(lines, np, P, couples, ncouple, V0);
 }
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout) {
   dim3 grid(nout, ML_EVENTS);
-  k_ml_reduce<<<grid, 64, 0, st>>>(Vin, nin, red, nout, Vout);
+  if (nout) k_ml_reduce<<<grid, 64, 0, st>>>(Vin, nin, red, nout, Vout);
 }
 void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial) {
-  k_ml_horner<<<nseg, 64, 0, st>>>(V, nseg, partial);
+  if (nseg) k_ml_horner<<<nseg, 64, 0, st>>>(V, nseg, partial);
 }
 
 }  // namespace gbls

@@ -68,9 +68,12 @@ __device__ void wg_reduce_jac(jac<F> &v) {
 }
 
 // level 1: workgroup c sums R[h*n + b .. h*n + e) (chunk table: {s, h, b, e}) and ORs the
-// bad flags (pk infinite -- blst PAIRING_Aggregate_PK_in_G1 -- or a failed pre-check)
+// bad flags: pk infinite (blst PAIRING_Aggregate_PK_in_G1), a zero scalar (the reference
+// only draws NonZeroU64, signature.rs:106-115; a zero would drop the set from the
+// combination, so it fails closed), or a failed pre-check
 __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32_t *chunks, uint32_t n,
-                                                      const g1a *pks, const int32_t *pre, g2j *part,
+                                                      const g1a *pks, const uint64_t *rands,
+                                                      const int32_t *pre, g2j *part,
                                                       int32_t *part_err) {
   __shared__ int32_t e_sh;
   uint32_t c = blockIdx.x;
@@ -83,7 +86,8 @@ __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32
   for (uint32_t i = b + threadIdx.x; i < e; i += WGR) {
     g2j r = R[(size_t)h * n + i];
     jac_add(acc, acc, r);
-    if (h == 0) bad |= (aff_is_inf(pks[i]) || (pre && pre[i] != 0)) ? 1 : 0;
+    if (h == 0)
+      bad |= (aff_is_inf(pks[i]) || (rands && rands[i] == 0) || (pre && pre[i] != 0)) ? 1 : 0;
   }
   if (bad) atomicOr(&e_sh, 1);
   wg_reduce_jac(acc);
@@ -101,7 +105,8 @@ __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32
 __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32_t *part_err,
                                                     const uint32_t *chunks, const uint32_t *seg_chunk,
                                                     const uint32_t *seg_off, uint32_t nseg, uint32_t n,
-                                                    g1a *P, g2a *H, int32_t *seg_err) {
+                                                    int empty_is_error, g1a *P, g2a *H,
+                                                    int32_t *seg_err) {
   constexpr int NQ = WG / 4;
   __shared__ g2j sh_lo[NQ], sh_hi[NQ];
   __shared__ int32_t sh_err[NQ];
@@ -136,7 +141,7 @@ __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32
     }
   }
   if (w != 0) return;
-  if (seg_off[s + 1] == seg_off[s]) err = 1;
+  if (empty_is_error && seg_off[s + 1] == seg_off[s]) err = 1;
   for (int j = 0; j < 32; j++) gang_dbl(hi, hi, q);
   gang_add(lo, lo, hi, q);
   g1a ng1;
@@ -151,18 +156,19 @@ __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32
 }
 
 void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1a *P) {
-  k_mv_g1mul<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
+  if (n) k_mv_g1mul<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
 }
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R) {
-  k_mv_g2mul<<<nblk(8 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
+  if (n) k_mv_g2mul<<<nblk(8 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
 }
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
-                  const g1a *pks, const int32_t *pre, g2j *part, int32_t *part_err, g1a *P, g2a *H,
-                  int32_t *seg_err) {
-  k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, pre, part, part_err);
-  k_g2sum_final<<<nseg, WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n, P, H,
-                                           seg_err);
+                  const g1a *pks, const uint64_t *rands, const int32_t *pre, int empty_is_error,
+                  g2j *part, int32_t *part_err, g1a *P, g2a *H, int32_t *seg_err) {
+  if (nchunks) k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, rands, pre, part, part_err);
+  if (nseg)
+    k_g2sum_final<<<nseg, WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n,
+                                       empty_is_error, P, H, seg_err);
 }
 
 }  // namespace gbls

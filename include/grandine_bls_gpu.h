@@ -18,19 +18,47 @@
  *   gbls_multi_verify           Signature::multi_verify               bls/src/signature.rs:95-129
  *                               (reached from MultiVerifier::finish, verifier.rs:301-323)
  *   gbls_multi_verify_segments  several independent multi_verify batches in one submission
+ *   gbls_multi_verify_bisect    per-set verdicts of a failed batch (replaces the per-item CPU
+ *                               fallbacks p2p/src/attestation_verifier.rs:228-240,373-386 and
+ *                               transition_functions/src/unphased/block_processing.rs:376-441)
+ *   gbls_registry_set           CachedPublicKey::decompress for a whole validator registry
+ *                               bls/src/cached_public_key.rs:104-108 (Validator.pubkey,
+ *                               types/src/phase0/containers.rs:229), device-resident
+ *   gbls_multi_verify_indexed   multi_verify / Triple::verify_aggregate over registry indices
+ *   gbls_g1_aggregate_indexed   AggregatePublicKey::aggregate over registry indices (e.g. the
+ *                               512-key get_next_sync_committee aggregate,
+ *                               helper_functions/src/accessors.rs:605-628)
+ *   gbls_g2_aggregate_segments  Signature::aggregate_in_place batched (op pools:
+ *                               operation_pools/src/attestation_agg_pool/tasks.rs:253,
+ *                               sync_committee_agg_pool/pool.rs:114,190)
+ *   gbls_fast_aggregate_verify_indexed  sync-committee fast_aggregate_verify over indices
+ *                               (operation_pools/src/sync_committee_agg_pool/tasks.rs:412-430)
  *   gbls_sk_to_pk / gbls_sign   SecretKey::to_public_key / sign       bls/src/secret_key.rs:74-86
+ *                               FIXTURE GENERATION ONLY: not constant time (the scalar
+ *                               multiplication branches on key bits); never sign with it.
  *
  * Conventions
  *   - gbls_p1_affine / gbls_p2_affine are byte-compatible with blst_p1_affine /
  *     blst_p2_affine: little-endian limbs in Montgomery form (R = 2^384); all-zero
  *     encodes the point at infinity.
  *   - Status codes mirror BLST_ERROR.  Verification entry points return
- *     GBLS_SUCCESS (valid) or GBLS_VERIFY_FAIL; any device/driver failure also
- *     returns GBLS_VERIFY_FAIL (fail closed) and sets gbls_last_error().
- *   - Host-pointer entry points are synchronous, reentrant and thread-safe; buffers
- *     are borrowed for the call only.  *_device variants take device pointers
- *     (inputs already resident in HBM) and are used by bench.py and the
- *     multi-GPU path.
+ *     GBLS_SUCCESS (valid) or GBLS_VERIFY_FAIL.  ANY engine/device/driver failure of
+ *     ANY entry point returns GBLS_VERIFY_FAIL (fail closed), fills verdict arrays
+ *     with GBLS_VERIFY_FAIL and status arrays with a failure code first, and sets the
+ *     thread-local gbls_last_error().
+ *   - Every entry point is reentrant and thread-safe: each call leases its own
+ *     streams and workspaces from a per-device pool.  Host-pointer entry points are
+ *     synchronous; buffers are borrowed for the call only.  *_device variants take
+ *     device pointers (inputs already resident in HBM), run on the calling thread's
+ *     current HIP device and are asynchronous on the given stream.
+ *   - gbls_init(device_mask, flags): one engine per set bit of device_mask (0: the
+ *     current device); flags & 0xff = engines per device (default 1; >1 lets tests
+ *     exercise the multi-device paths on one GPU).  Host-pointer calls shard large
+ *     batches over the engines: whole segments per engine, or per-engine Miller
+ *     partials of one batch combined by a single final exponentiation.
+ *   - Segment offsets must satisfy seg_off[0] == 0, seg_off[i] <= seg_off[i+1] and
+ *     seg_off[nseg] == n (else GBLS_ERR_ARG).
+ *   - A zero random scalar fails its batch (the reference only draws NonZeroU64).
  *   - There is NO CPU fallback inside this library: without a usable gfx950 device
  *     every call fails with GBLS_ERR_NO_DEVICE.
  */
@@ -75,6 +103,7 @@ enum {
 int gbls_init(uint32_t device_mask, uint32_t flags);
 int gbls_last_error(void);
 const char *gbls_version(void);
+int gbls_device_count(void); /* engines (devices x replicas) after gbls_init; 0 before */
 
 /* a9 / a8 / a10 */
 int gbls_g1_decompress(const uint8_t (*in)[48], size_t n, int validate, gbls_p1_affine *out,
@@ -89,6 +118,18 @@ int gbls_g1_aggregate(const gbls_p1_affine *pks, size_t n, gbls_p1_affine *out);
 int gbls_g1_aggregate_segments(const gbls_p1_affine *pks, const uint32_t *seg_offsets, size_t nseg,
                                gbls_p1_affine *out, int32_t *status);
 int gbls_g2_aggregate(const gbls_p2_affine *sigs, size_t n, gbls_p2_affine *out);
+int gbls_g2_aggregate_segments(const gbls_p2_affine *sigs, const uint32_t *seg_offsets,
+                               size_t nseg, gbls_p2_affine *out, int32_t *status);
+
+/* f1: device-resident validator registry.  gbls_registry_set decompresses and validates
+ * (PublicKey::try_from semantics) keys [first, first + n) on every engine device;
+ * invalid keys are stored as infinity (rejected by every verification) and reported in
+ * status.  The registry grows as needed; indices past its size are BAD_ENCODING. */
+int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t *status);
+size_t gbls_registry_size(void);
+/* sum of registry keys idx[seg_offsets[s] .. seg_offsets[s+1]) per segment */
+int gbls_g1_aggregate_indexed(const uint32_t *idx, const uint32_t *seg_offsets, size_t nseg,
+                              gbls_p1_affine *out, int32_t *status);
 
 /* a6 / a7: returns GBLS_SUCCESS iff the signature verifies (blst semantics:
  * sig_groupcheck = true, pk_validate = false, infinite pk rejected). */
@@ -106,6 +147,12 @@ int gbls_fast_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *
                                      const uint32_t *msg_off, const gbls_p1_affine *pks,
                                      const uint32_t *seg_off, size_t m, int32_t *verdicts);
 
+/* sync-committee shape over the registry: message i is checked against the aggregate of
+ * registry keys pk_idx[seg_off[i] .. seg_off[i+1]) */
+int gbls_fast_aggregate_verify_indexed(const gbls_p2_affine *sigs, const uint8_t *msg_data,
+                                       const uint32_t *msg_off, const uint32_t *pk_idx,
+                                       const uint32_t *seg_off, size_t m, int32_t *verdicts);
+
 /* a1: random-linear-combination batch verification with caller-supplied nonzero
  * 64-bit scalars (bls/src/signature.rs:106-115 draws them); n == 0 -> VERIFY_FAIL
  * (MultiVerifier::finish short-circuits n == 0 before calling, verifier.rs:303-305). */
@@ -116,21 +163,51 @@ int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *
                                const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                const uint32_t *seg_off, size_t nseg, int32_t *verdicts);
 
+/* a1 + a4 over the registry: set i's key = registry[pk_idx[i]] (pk_off == NULL) or the
+ * aggregate of registry[pk_idx[pk_off[i] .. pk_off[i+1])] (Triple::verify_aggregate). */
+int gbls_multi_verify_indexed(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
+                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                              const uint64_t *rands, size_t n);
+/* f2: per-set verdicts (GBLS_SUCCESS / GBLS_VERIFY_FAIL, as each set would fare in
+ * multi_verify alone) by GPU bisection: the batch, then rounds that split every failing
+ * range 16 ways and verify all pieces as segments of one submission.  Keys come from
+ * pks (points) or, when pks == NULL, from the registry as in gbls_multi_verify_indexed. */
+int gbls_multi_verify_bisect(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
+                             const gbls_p1_affine *pks, const uint32_t *pk_idx,
+                             const uint32_t *pk_off, const uint64_t *rands, size_t n,
+                             int32_t *set_verdicts);
+
 /* Device-pointer variants: inputs, outputs, verdicts and partials are device memory
  * (already resident in HBM); seg_off is a HOST array of nseg + 1 offsets (it sets the
- * launch geometry).  stream may be NULL (the library's own stream).  Asynchronous:
- * the caller synchronises the stream. */
+ * launch geometry).  Asynchronous on `stream` (NULL = the legacy default stream, which
+ * orders with PyTorch's default stream): the caller synchronises the stream. */
 int gbls_multi_verify_segments_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
                                       const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                       const uint32_t *seg_off, size_t nseg, int32_t *verdicts,
                                       void *stream);
+/* registry-indexed: pk_idx / pk_off (may be NULL) are device arrays */
+int gbls_multi_verify_indexed_segments_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
+                                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                                              const uint64_t *rands, size_t n,
+                                              const uint32_t *seg_off, size_t nseg,
+                                              int32_t *verdicts, void *stream);
 /* Multi-GPU split: per-segment Miller partial  F_s = prod_i ML(r_i pk_i, H(m_i)) * ML(-g1, S_s)
  * (no final exponentiation) + per-segment error flags; then the product of k partials
- * per segment and one final exponentiation. */
+ * per segment and one final exponentiation.  An empty segment's partial is the identity
+ * with no error (a shard may receive no sets); partials are laid out [part][segment]. */
+int gbls_fast_aggregate_verify_indexed_device(const gbls_p2_affine *sigs, const uint8_t *msgs,
+                                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                                              size_t m, int32_t *verdicts, void *stream);
 int gbls_multi_verify_partials_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
                                       const gbls_p1_affine *pks, const uint64_t *rands, size_t n,
                                       const uint32_t *seg_off, size_t nseg, gbls_fp12 *partials,
                                       int32_t *seg_err, void *stream);
+int gbls_multi_verify_indexed_partials_device(const uint8_t *msgs, const gbls_p2_affine *sigs,
+                                              const uint32_t *pk_idx, const uint32_t *pk_off,
+                                              const uint64_t *rands, size_t n,
+                                              const uint32_t *seg_off, size_t nseg,
+                                              gbls_fp12 *partials, int32_t *seg_err,
+                                              void *stream);
 int gbls_final_verify_partials_device(const gbls_fp12 *partials, const int32_t *seg_err,
                                       size_t nparts, size_t nseg, int32_t *verdicts, void *stream);
 

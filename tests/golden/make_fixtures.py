@@ -283,6 +283,21 @@ def main():
     mcase(list(range(4)), pk_over={1: None}, note="infinite public key")
     mcase([0, 1], sig_over={0: sigs[1], 1: sigs[0]}, note="signatures swapped between sets")
     mcase([7, 7, 8], note="duplicate set")
+    # SURVEY 8(a) verdict contract 4 and 6: no G2 group check of sigma in multi_verify,
+    # infinite sigma skipped in the G2 sum
+    mcase([0, 1, 2], sig_over={1: None}, note="infinite signature")
+    mcase([0, 1, 2], sig_over={2: bad_sig}, note="signature on the curve, not in G2")
+    r = rng.randrange(1, 1 << 64)
+    m0 = msgs[3]
+    mv.append({"msgs": [m0.hex(), m0.hex()], "sigs": [g2hex(None), g2hex(None)],
+               "pks": [g1hex(pks[3]), g1hex(O.g1_neg(pks[3]))], "rands": [str(r), str(r)],
+               "expect": O.multi_verify([m0, m0], [None, None], [pks[3], O.g1_neg(pks[3])], [r, r]),
+               "note": "infinite signatures, keys cancel under equal scalars"})
+    r2 = rng.randrange(1, 1 << 64)
+    mv.append({"msgs": [m0.hex(), m0.hex()], "sigs": [g2hex(None), g2hex(None)],
+               "pks": [g1hex(pks[3]), g1hex(O.g1_neg(pks[3]))], "rands": [str(r), str(r2)],
+               "expect": O.multi_verify([m0, m0], [None, None], [pks[3], O.g1_neg(pks[3])], [r, r2]),
+               "note": "infinite signatures, keys do not cancel under distinct scalars"})
     out["multi_verify"] = {"provenance": "oracle (Signature::multi_verify, signature.rs:95-129; fixed scalars)",
                            "cases": mv}
 
