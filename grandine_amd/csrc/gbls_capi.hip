@@ -124,15 +124,15 @@ struct StageTimer {  // RAII: events around one stage's launches when profiling
 struct Ctx {
   int hipdev = -1;
   hipStream_t own = nullptr, side1 = nullptr, side2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_done = nullptr,
-             ev_upl = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
+             ev_done = nullptr, ev_upl = nullptr;
   bool done_pending = false, upl_pending = false;
   bool active = false;                // a call holds the lease and has begun
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
   Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, gpart, lines, V0, V1, tab, part, err, out0,
-      out1, pks, pre;
+      out1, pks, pre, pre2;
   void *stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
   std::vector<uint32_t> host_tab;  // table assembly, reused across calls
@@ -146,6 +146,7 @@ struct Ctx {
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side1, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side2, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_pks, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_upl, hipEventDisableTiming));
     return true;
@@ -237,6 +238,7 @@ struct Engine {
   std::atomic<uint32_t> rr{0};
   std::shared_mutex reg_mu;
   size_t reg_n = 0;
+  std::atomic<bool> coalesce{true};
 } g;
 
 // RAII lease of a context of one device: the idle context last used on the caller's
@@ -313,6 +315,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     ids.push_back(cur);
   }
   if (ids.empty()) return fail(GBLS_ERR_NO_DEVICE);
+  g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
   for (int id : ids) {
@@ -349,15 +352,57 @@ bool valid_offsets(const uint32_t *off, size_t nseg, size_t n) {
   return true;
 }
 
+// ----- where a batch's public keys come from (device pointers inside the pipeline)
+struct PkSource {
+  const g1a *pts = nullptr;       // points: one per set (off == nullptr) or summed per set
+  const uint32_t *idx = nullptr;  // registry indices: one per set (off == nullptr) or summed
+  const uint32_t *off = nullptr;  // per-set ranges [off[i], off[i+1]) of pts / idx
+};
+
+// Resolve a DEVICE key source into per-set affine keys on stream st; *pre = per-set
+// status (nonzero = reject: empty aggregate, index out of range) or nullptr.  The caller
+// holds the registry lock (shared) while it enqueues.
+bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t st,
+                 const g1a **pks, const int32_t **pre) {
+  *pre = nullptr;
+  if ((src.pts && !src.off) || n == 0) {
+    *pks = src.pts;
+    return true;
+  }
+  if (!src.pts && !src.idx) return fail(GBLS_ERR_ARG);
+  if (!c.ensure(c.pks, n * sizeof(g1a)) || !c.ensure(c.pre, n * sizeof(int32_t))) return false;
+  StageTimer t(S_PK_GATHER, st);
+  const g1a *reg = d.reg.as<g1a>();
+  if (src.pts)
+    launch_g1_aggregate_seg(st, src.pts, src.off, (uint32_t)n, c.pks.as<g1a>(),
+                            c.pre.as<int32_t>());
+  else if (src.off)
+    launch_g1_aggregate_idx(st, reg, (uint32_t)g.reg_n, src.idx, src.off, (uint32_t)n,
+                            c.pks.as<g1a>(), c.pre.as<int32_t>());
+  else
+    launch_g1_gather_idx(st, reg, (uint32_t)g.reg_n, src.idx, (uint32_t)n, c.pks.as<g1a>(),
+                         c.pre.as<int32_t>());
+  *pks = c.pks.as<g1a>();
+  *pre = c.pre.as<int32_t>();
+  return true;
+}
+
 // ----- the verification pipeline on device pointers.
 // Sets [0, n) grouped in segments by seg_off (HOST array, nseg + 1 entries); per segment
 // a Miller partial (no final exponentiation) and an error flag.  rands == nullptr
-// means r_i = 1 (single checks); pre[i] != 0 marks a set that failed a pre-check.
-bool pipeline_partials(Ctx &c, const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
-                       const g1a *pks, const uint64_t *rands, const int32_t *pre, size_t n,
-                       const uint32_t *seg_off, size_t nseg, int empty_is_error, fp12 *partials,
-                       int32_t *seg_err, hipStream_t st) {
+// means r_i = 1 (single checks); sig_groupcheck adds the G2 subgroup check of every
+// signature (verify / fast_aggregate_verify, signature.rs:51,86).  Streams:
+//   side 1: key resolution (gather / aggregation) -> r_i pk_i
+//   side 2: signature group check, then S = sum r_i sig_i (waits for the keys' flags),
+//           then the lines of the (-g1, S) pairs
+//   main:   hash_to_G2 -> the sets' lines;  join -> Miller product tree -> partials
+bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *msg_off,
+                       const g2a *sigs, const PkSource &src, const uint64_t *rands,
+                       bool sig_groupcheck, size_t n, const uint32_t *seg_off, size_t nseg,
+                       int empty_is_error, fp12 *partials, int32_t *seg_err, hipStream_t st) {
   const size_t np = n + nseg;
+  bool single = !rands && n == nseg;  // one set per segment, r = 1
+  for (size_t s = 0; single && s <= nseg; s++) single = seg_off[s] == s;
   // ---- host tables, one staged upload:
   //   [couples][g2 chunks][seg_chunk][reduction levels][seg_off]
   std::vector<uint32_t> &tab = c.host_tab;
@@ -426,6 +471,7 @@ bool pipeline_partials(Ctx &c, const uint8_t *msgs, const uint32_t *msg_off, con
   size_t v1_n = 1, v0_n = ncouple;
   for (size_t l = 0; l < levels.size(); l++)
     (l & 1 ? v0_n : v1_n) = std::max(l & 1 ? v0_n : v1_n, levels[l].nout);
+  if (sig_groupcheck && !c.ensure(c.pre2, n * sizeof(int32_t) + 16)) return false;
   if (!c.ensure(c.U, 2 * n * sizeof(fp2) + 16) || !c.ensure(c.Q, 2 * n * sizeof(g2j) + 16) ||
       !c.ensure(c.H, np * sizeof(g2a)) || !c.ensure(c.P, np * sizeof(g1a)) ||
       !c.ensure(c.R, 2 * n * sizeof(g2j) + 16) ||
@@ -438,24 +484,36 @@ bool pipeline_partials(Ctx &c, const uint8_t *msgs, const uint32_t *msg_off, con
   const uint32_t *T = c.tab.as<uint32_t>();
   g2j *gpart = c.gpart.as<g2j>();
   int32_t *gpart_err = reinterpret_cast<int32_t *>(gpart + nchunks);
-  // ---- fork: side stream 1 = G1 scalar products, side stream 2 = G2 sum + its lines,
-  // main stream = hash_to_G2 + the sets' lines; join before the Miller tree.
+  // ---- fork
   HIPCHK(hipEventRecord(c.ev_fork, st));
   HIPCHK(hipStreamWaitEvent(c.side1, c.ev_fork, 0));
   HIPCHK(hipStreamWaitEvent(c.side2, c.ev_fork, 0));
+  const g1a *pks = nullptr;
+  const int32_t *pre = nullptr;
+  if (!resolve_pks(c, d, src, n, c.side1, &pks, &pre)) return false;
+  HIPCHK(hipEventRecord(c.ev_pks, c.side1));
   {
     StageTimer t(S_G1MUL, c.side1);
     launch_mv_g1mul(c.side1, pks, rands, N, c.P.as<g1a>());
   }
-  {
+  const int32_t *pre2 = nullptr;
+  if (sig_groupcheck) {
+    launch_g2_check(c.side2, sigs, N, c.pre2.as<int32_t>(), 0);
+    pre2 = c.pre2.as<int32_t>();
+  }
+  if (!single) {
     StageTimer t(S_G2MUL, c.side2);
     launch_mv_g2mul(c.side2, sigs, rands, N, c.R.as<g2j>());
   }
+  HIPCHK(hipStreamWaitEvent(c.side2, c.ev_pks, 0));
   {
     StageTimer t(S_G2SUM, c.side2);
-    launch_g2sum(c.side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
-                 T + segoff_at, NS, N, pks, rands, pre, empty_is_error, gpart, gpart_err,
-                 c.P.as<g1a>(), c.H.as<g2a>(), seg_err);
+    if (single)
+      launch_single_S(c.side2, sigs, pks, pre, pre2, N, c.P.as<g1a>(), c.H.as<g2a>(), seg_err);
+    else
+      launch_g2sum(c.side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
+                   T + segoff_at, NS, N, pks, rands, pre, pre2, empty_is_error, gpart, gpart_err,
+                   c.P.as<g1a>(), c.H.as<g2a>(), seg_err);
   }
   {
     StageTimer t(S_LINES_S, c.side2);
@@ -511,71 +569,44 @@ bool pipeline_final(const fp12 *partials, const int32_t *err, size_t nparts, siz
   return true;
 }
 
-bool pipeline_verdicts(Ctx &c, const uint8_t *msgs, const uint32_t *msg_off, const g2a *sigs,
-                       const g1a *pks, const uint64_t *rands, const int32_t *pre, size_t n,
-                       const uint32_t *seg_off, size_t nseg, int32_t *verdicts, hipStream_t st) {
+bool pipeline_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *msg_off,
+                       const g2a *sigs, const PkSource &src, const uint64_t *rands,
+                       bool sig_groupcheck, size_t n, const uint32_t *seg_off, size_t nseg,
+                       int32_t *verdicts, hipStream_t st) {
   if (!c.ensure(c.part, nseg * sizeof(fp12)) || !c.ensure(c.err, nseg * sizeof(int32_t) + 16))
     return false;
-  return pipeline_partials(c, msgs, msg_off, sigs, pks, rands, pre, n, seg_off, nseg, 1,
-                           c.part.as<fp12>(), c.err.as<int32_t>(), st) &&
+  return pipeline_partials(c, d, msgs, msg_off, sigs, src, rands, sig_groupcheck, n, seg_off, nseg,
+                           1, c.part.as<fp12>(), c.err.as<int32_t>(), st) &&
          pipeline_final(c.part.as<fp12>(), c.err.as<int32_t>(), 1, nseg, verdicts, st);
 }
 
-// ----- where a batch's public keys come from
-struct PkSource {
-  const g1a *pts = nullptr;       // one point per set, or
-  const uint32_t *idx = nullptr;  // registry indices: one per set (off == nullptr), or
-  const uint32_t *off = nullptr;  // the sum of idx[off[i] .. off[i+1]) per set
-};
-
-// Resolve a DEVICE-side key source into per-set affine keys (+ pre flags) on the device.
-// The caller holds the registry lock (shared) while it enqueues.
-bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t st,
-                 const g1a **pks, const int32_t **pre) {
-  *pre = nullptr;
-  if (src.pts || n == 0) {
-    *pks = src.pts;
-    return true;
-  }
-  if (!src.idx) return fail(GBLS_ERR_ARG);
-  if (!c.ensure(c.pks, n * sizeof(g1a)) || !c.ensure(c.pre, n * sizeof(int32_t))) return false;
-  StageTimer t(S_PK_GATHER, st);
-  const g1a *reg = d.reg.as<g1a>();
-  if (src.off)
-    launch_g1_aggregate_idx(st, reg, (uint32_t)g.reg_n, src.idx, src.off, (uint32_t)n,
-                            c.pks.as<g1a>(), c.pre.as<int32_t>());
-  else
-    launch_g1_gather_idx(st, reg, (uint32_t)g.reg_n, src.idx, (uint32_t)n, c.pks.as<g1a>(),
-                         c.pre.as<int32_t>());
-  *pks = c.pks.as<g1a>();
-  *pre = c.pre.as<int32_t>();
-  return true;
-}
-
-// Upload a HOST key source for sets [b, e) and resolve it on the device.
-bool upload_pks(Ctx &c, Device &d, const PkSource &host, size_t b, size_t e, hipStream_t st,
-                const g1a **pks, const int32_t **pre) {
+// Upload a HOST key source for sets [b, e) as a device key source.
+bool upload_pks(Ctx &c, const PkSource &host, size_t b, size_t e, hipStream_t st, PkSource *dev) {
   size_t n = e - b;
-  PkSource dev;
-  if (host.pts) {
-    if (!c.upload_staged(c.in2, host.pts + b, n * sizeof(g1a), st)) return false;
-    dev.pts = c.in2.as<g1a>();
-  } else if (host.off) {
+  *dev = PkSource();
+  if (host.off) {
     uint32_t base = host.off[b], cnt = host.off[e] - base;
     std::vector<uint32_t> off(n + 1);
     for (size_t i = 0; i <= n; i++) off[i] = host.off[b + i] - base;
-    if (!c.upload_staged(c.in2, host.idx + base, (size_t)cnt * 4, st) ||
-        !c.upload_staged(c.in5, off.data(), (n + 1) * 4, st))
-      return false;
-    dev.idx = c.in2.as<uint32_t>();
-    dev.off = c.in5.as<uint32_t>();
+    if (!c.upload_staged(c.in5, off.data(), (n + 1) * 4, st)) return false;
+    dev->off = c.in5.as<uint32_t>();
+    if (host.pts) {
+      if (!c.upload_staged(c.in2, host.pts + base, (size_t)cnt * sizeof(g1a), st)) return false;
+      dev->pts = c.in2.as<g1a>();
+    } else {
+      if (!c.upload_staged(c.in2, host.idx + base, (size_t)cnt * 4, st)) return false;
+      dev->idx = c.in2.as<uint32_t>();
+    }
+  } else if (host.pts) {
+    if (!c.upload_staged(c.in2, host.pts + b, n * sizeof(g1a), st)) return false;
+    dev->pts = c.in2.as<g1a>();
   } else if (host.idx) {
     if (!c.upload_staged(c.in2, host.idx + b, n * 4, st)) return false;
-    dev.idx = c.in2.as<uint32_t>();
+    dev->idx = c.in2.as<uint32_t>();
   } else {
     return fail(GBLS_ERR_ARG);
   }
-  return resolve_pks(c, d, dev, n, st, pks, pre);
+  return true;
 }
 
 // One device: host batch [sets b..e) in segments seg (rebased, host) -> per-segment
@@ -592,19 +623,18 @@ bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
       !c.upload_staged(c.in1, sigs + b, n * sizeof(g2a), st) ||
       !c.upload_staged(c.in3, rands + b, n * 8, st))
     return false;
-  const g1a *pks = nullptr;
-  const int32_t *pre = nullptr;
-  if (!upload_pks(c, d, src, b, e, st, &pks, &pre)) return false;
+  PkSource dsrc;
+  if (!upload_pks(c, src, b, e, st, &dsrc)) return false;
   if (verdicts) {
     if (!c.ensure(c.out1, nseg * sizeof(int32_t))) return false;
-    if (!pipeline_verdicts(c, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), pks,
-                           c.in3.as<uint64_t>(), pre, n, seg, nseg, c.out1.as<int32_t>(), st))
+    if (!pipeline_verdicts(c, d, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), dsrc,
+                           c.in3.as<uint64_t>(), false, n, seg, nseg, c.out1.as<int32_t>(), st))
       return false;
     HIPCHK(hipMemcpyAsync(verdicts, c.out1.p, nseg * 4, hipMemcpyDeviceToHost, st));
   } else {
     if (!c.ensure(c.part, sizeof(fp12)) || !c.ensure(c.err, 16)) return false;
-    if (!pipeline_partials(c, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), pks,
-                           c.in3.as<uint64_t>(), pre, n, seg, 1, 0, c.part.as<fp12>(),
+    if (!pipeline_partials(c, d, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), dsrc,
+                           c.in3.as<uint64_t>(), false, n, seg, 1, 0, c.part.as<fp12>(),
                            c.err.as<int32_t>(), st))
       return false;
     HIPCHK(hipMemcpyAsync(part_host, c.part.p, sizeof(fp12), hipMemcpyDeviceToHost, st));
@@ -680,6 +710,141 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
   for (auto &L : leases)
     if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
   return ok;
+}
+
+// ----- f3: cross-caller coalescing.  Concurrent host-pointer multi_verify calls (the
+// node's gossip batches of <= 64 sets, p2p/src/attestation_verifier.rs:37,142-163, and
+// the block verification pool's per-block batches, p2p/src/block_verification_pool.rs:
+// 103-128) queue here; a caller that finds fewer than kLeadersPerDevice x devices
+// submissions in flight becomes a leader and verifies every queued request with the same
+// key source kind as ONE segmented submission (each request keeps its own segments and
+// verdicts).  Batches therefore grow with the load, while an idle engine runs a lone
+// call immediately (no waiting window).
+constexpr int kLeadersPerDevice = 2;
+constexpr size_t kMaxMergedSets = 1 << 20;
+
+struct CoReq {
+  const uint8_t *msgs;
+  const g2a *sigs;
+  PkSource src;  // host pointers
+  const uint64_t *rands;
+  size_t n;
+  const uint32_t *seg_off;
+  size_t nseg;
+  int32_t *verdicts;
+  bool done = false, ok = false;
+  int err = GBLS_ERR_NONE;
+  int kind() const { return (src.pts ? 1 : 0) | (src.off ? 2 : 0); }
+  size_t nkeys() const { return src.off ? src.off[n] : n; }
+};
+
+struct Coalescer {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<CoReq *> q;
+  int leaders = 0;
+} co;
+
+bool verify_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
+                 const uint64_t *rands, size_t n, const uint32_t *seg_off, size_t nseg,
+                 int32_t *verdicts);
+
+void run_merged(std::vector<CoReq *> &batch) {
+  if (batch.size() == 1) {
+    CoReq &r = *batch[0];
+    r.ok = verify_host(r.msgs, r.sigs, r.src, r.rands, r.n, r.seg_off, r.nseg, r.verdicts);
+    r.err = t_last_error;
+    r.done = true;
+    return;
+  }
+  size_t n = 0, nseg = 0, nk = 0;
+  for (CoReq *r : batch) {
+    n += r->n;
+    nseg += r->nseg;
+    nk += r->nkeys();
+  }
+  const CoReq &r0 = *batch[0];
+  std::vector<uint8_t> msgs(32 * n);
+  std::vector<g2a> sigs(n);
+  std::vector<uint64_t> rands(n);
+  std::vector<g1a> pts;
+  std::vector<uint32_t> idx, off, seg(nseg + 1);
+  if (r0.src.pts) pts.resize(nk);
+  else idx.resize(nk);
+  if (r0.src.off) off.resize(n + 1);
+  std::vector<int32_t> v(nseg, GBLS_VERIFY_FAIL);
+  size_t at = 0, sat = 0, kat = 0;
+  seg[0] = 0;
+  for (CoReq *r : batch) {
+    std::memcpy(&msgs[32 * at], r->msgs, 32 * r->n);
+    std::memcpy(&sigs[at], r->sigs, r->n * sizeof(g2a));
+    std::memcpy(&rands[at], r->rands, r->n * 8);
+    size_t k = r->nkeys();
+    if (r0.src.pts) std::memcpy(&pts[kat], r->src.pts, k * sizeof(g1a));
+    else std::memcpy(&idx[kat], r->src.idx, k * 4);
+    if (r0.src.off)
+      for (size_t i = 0; i <= r->n; i++) off[at + i] = (uint32_t)(kat + r->src.off[i]);
+    for (size_t s = 1; s <= r->nseg; s++) seg[sat + s] = (uint32_t)(at + r->seg_off[s]);
+    at += r->n;
+    sat += r->nseg;
+    kat += k;
+  }
+  PkSource src;
+  if (r0.src.pts) src.pts = pts.data();
+  else src.idx = idx.data();
+  if (r0.src.off) src.off = off.data();
+  bool ok = verify_host(msgs.data(), sigs.data(), src, rands.data(), n, seg.data(), nseg, v.data());
+  int err = t_last_error;
+  sat = 0;
+  for (CoReq *r : batch) {
+    std::memcpy(r->verdicts, &v[sat], r->nseg * 4);
+    sat += r->nseg;
+    r->ok = ok;
+    r->err = err;
+    r->done = true;
+  }
+}
+
+bool coalesced_verify(CoReq &r) {
+  if (!g.coalesce.load()) {
+    bool ok = verify_host(r.msgs, r.sigs, r.src, r.rands, r.n, r.seg_off, r.nseg, r.verdicts);
+    return ok;
+  }
+  const int max_leaders = kLeadersPerDevice * (int)g.devs.size();
+  std::unique_lock<std::mutex> lk(co.mu);
+  co.q.push_back(&r);
+  while (!r.done) {
+    if (co.leaders < max_leaders && !co.q.empty()) {
+      co.leaders++;
+      std::vector<CoReq *> batch;
+      auto mine = std::find(co.q.begin(), co.q.end(), &r);
+      int kind = mine != co.q.end() ? r.kind() : co.q.front()->kind();
+      size_t sets = 0;
+      if (mine != co.q.end()) {
+        batch.push_back(&r);
+        sets = r.n;
+        co.q.erase(mine);
+      }
+      for (auto it = co.q.begin(); it != co.q.end();) {
+        if ((*it)->kind() == kind && (batch.empty() || sets + (*it)->n <= kMaxMergedSets)) {
+          sets += (*it)->n;
+          batch.push_back(*it);
+          it = co.q.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      lk.unlock();
+      run_merged(batch);
+      lk.lock();
+      co.leaders--;
+      co.cv.notify_all();
+    } else {
+      co.cv.wait(lk);
+    }
+  }
+  t_last_error = r.err;
+  return r.ok;
 }
 
 void fill(int32_t *v, size_t n, int32_t x) {
@@ -933,9 +1098,8 @@ int gbls_g2_aggregate(const gbls_p2_affine *sigs, size_t n, gbls_p2_affine *out)
 }
 
 // m independent checks e(pk_i, H(m_i)) == e(g1, sig_i), each its own segment (r_i = 1),
-// with the signature subgroup check (and, for FAV, the key aggregation status) folded
-// into the pre-flags.  mode 0: one key per check (pts); 1: aggregate pts per check
-// (seg_off); 2: aggregate registry keys idx per check (seg_off).
+// with the signature subgroup check.  mode 0: one key per check (pts); 1: aggregate pts
+// per check (seg_off); 2: aggregate registry keys idx per check (seg_off).
 static int single_checks(const g2a *sigs, const uint8_t *msg_data, const uint32_t *msg_off,
                          const void *keys, const uint32_t *seg_off, size_t m, int mode,
                          int32_t *verdicts) {
@@ -955,29 +1119,20 @@ static int single_checks(const g2a *sigs, const uint8_t *msg_data, const uint32_
   if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, sigs, m * sizeof(g2a), st) ||
       !c.upload_staged(c.in1, msg_data, msg_off[m] ? msg_off[m] : 1, st) ||
       !c.upload_staged(c.in2, msg_off, (m + 1) * 4, st) ||
-      !c.upload_staged(c.in4, keys, nkeys * (mode == 2 ? 4 : sizeof(g1a)), st) ||
-      !c.ensure(c.in3, m * sizeof(g1a)) || !c.ensure(c.out0, m * sizeof(int32_t)) ||
+      !c.upload_staged(c.in4, keys, (nkeys ? nkeys : 1) * (mode == 2 ? 4 : sizeof(g1a)), st) ||
       !c.ensure(c.out1, m * sizeof(int32_t)))
     return FAILED;
-  const g1a *pks;
-  if (mode == 0) {
-    pks = c.in4.as<g1a>();
-    if (hipMemsetAsync(c.out0.p, 0, m * 4, st) != hipSuccess) return fail(GBLS_ERR_HIP), FAILED;
-  } else {
+  PkSource src;
+  if (mode == 2)
+    src.idx = c.in4.as<uint32_t>();
+  else
+    src.pts = c.in4.as<g1a>();
+  if (mode) {
     if (!c.upload_staged(c.in5, seg_off, (m + 1) * 4, st)) return FAILED;
-    if (mode == 1)
-      launch_g1_aggregate_seg(st, c.in4.as<g1a>(), c.in5.as<uint32_t>(), (uint32_t)m,
-                              c.in3.as<g1a>(), c.out0.as<int32_t>());
-    else
-      launch_g1_aggregate_idx(st, d.reg.as<g1a>(), (uint32_t)g.reg_n, c.in4.as<uint32_t>(),
-                              c.in5.as<uint32_t>(), (uint32_t)m, c.in3.as<g1a>(),
-                              c.out0.as<int32_t>());
-    pks = c.in3.as<g1a>();
+    src.off = c.in5.as<uint32_t>();
   }
-  launch_g2_check(st, c.in0.as<g2a>(), (uint32_t)m, c.out0.as<int32_t>(), 1);
-  if (!pipeline_verdicts(c, c.in1.as<uint8_t>(), c.in2.as<uint32_t>(), c.in0.as<g2a>(), pks,
-                         nullptr, c.out0.as<int32_t>(), m, ident.data(), m, c.out1.as<int32_t>(),
-                         st))
+  if (!pipeline_verdicts(c, d, c.in1.as<uint8_t>(), c.in2.as<uint32_t>(), c.in0.as<g2a>(), src,
+                         nullptr, true, m, ident.data(), m, c.out1.as<int32_t>(), st))
     return FAILED;
   if (hipMemcpyAsync(verdicts, c.out1.p, m * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess) {
@@ -1038,10 +1193,10 @@ int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *
   API_BEGIN
   if (nseg == 0) return GBLS_SUCCESS;
   if (!valid_offsets(seg_off, nseg, n)) return fail(GBLS_ERR_ARG), FAILED;
-  PkSource src;
-  src.pts = reinterpret_cast<const g1a *>(pks);
-  if (!verify_host(&msgs[0][0], reinterpret_cast<const g2a *>(sigs), src, rands, n, seg_off, nseg,
-                   verdicts)) {
+  CoReq r{&msgs[0][0], reinterpret_cast<const g2a *>(sigs), PkSource(), rands, n, seg_off,
+          nseg, verdicts};
+  r.src.pts = reinterpret_cast<const g1a *>(pks);
+  if (!coalesced_verify(r)) {
     fill(verdicts, nseg, GBLS_VERIFY_FAIL);
     return FAILED;
   }
@@ -1066,13 +1221,12 @@ int gbls_multi_verify_indexed(const uint8_t (*msgs)[32], const gbls_p2_affine *s
   API_BEGIN
   if (n == 0) return GBLS_VERIFY_FAIL;
   if (pk_off && !valid_offsets(pk_off, n, pk_off[n])) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
-  PkSource src;
-  src.idx = pk_idx;
-  src.off = pk_off;
   uint32_t off[2] = {0, (uint32_t)n};
   int32_t v = GBLS_VERIFY_FAIL;
-  if (!verify_host(&msgs[0][0], reinterpret_cast<const g2a *>(sigs), src, rands, n, off, 1, &v))
-    return GBLS_VERIFY_FAIL;
+  CoReq r{&msgs[0][0], reinterpret_cast<const g2a *>(sigs), PkSource(), rands, n, off, 1, &v};
+  r.src.idx = pk_idx;
+  r.src.off = pk_off;
+  if (!coalesced_verify(r)) return GBLS_VERIFY_FAIL;
   return v;
 }
 
@@ -1111,13 +1265,10 @@ static int device_verify(const uint8_t *msgs, const g2a *sigs, const PkSource &s
   Ctx &c = *L;
   hipStream_t st = (hipStream_t)stream;
   if (!L.ok() || !c.begin(st)) return FAILED;
-  const g1a *pks = nullptr;
-  const int32_t *pre = nullptr;
-  if (!resolve_pks(c, *d, src, n, st, &pks, &pre)) return FAILED;
-  bool ok = verdicts ? pipeline_verdicts(c, msgs, nullptr, sigs, pks, rands, pre, n, seg_off, nseg,
-                                         verdicts, st)
-                     : pipeline_partials(c, msgs, nullptr, sigs, pks, rands, pre, n, seg_off,
-                                         nseg, 0, partials, seg_err, st);
+  bool ok = verdicts ? pipeline_verdicts(c, *d, msgs, nullptr, sigs, src, rands, false, n, seg_off,
+                                         nseg, verdicts, st)
+                     : pipeline_partials(c, *d, msgs, nullptr, sigs, src, rands, false, n,
+                                         seg_off, nseg, 0, partials, seg_err, st);
   return ok ? GBLS_SUCCESS : FAILED;
 }
 
@@ -1197,18 +1348,12 @@ int gbls_fast_aggregate_verify_indexed_device(const gbls_p2_affine *sigs, const 
   hipStream_t st = (hipStream_t)stream;
   std::vector<uint32_t> ident(m + 1);
   for (size_t i = 0; i <= m; i++) ident[i] = (uint32_t)i;
-  if (!L.ok() || !c.begin(st) || !c.ensure(c.in3, m * sizeof(g1a)) ||
-      !c.ensure(c.out0, m * sizeof(int32_t)))
-    return FAILED;
-  {
-    StageTimer t(S_PK_GATHER, st);
-    launch_g1_aggregate_idx(st, d->reg.as<g1a>(), (uint32_t)g.reg_n, pk_idx, pk_off, (uint32_t)m,
-                            c.in3.as<g1a>(), c.out0.as<int32_t>());
-  }
-  const g2a *sg = reinterpret_cast<const g2a *>(sigs);
-  launch_g2_check(st, sg, (uint32_t)m, c.out0.as<int32_t>(), 1);
-  return pipeline_verdicts(c, msgs, nullptr, sg, c.in3.as<g1a>(), nullptr, c.out0.as<int32_t>(), m,
-                           ident.data(), m, verdicts, st)
+  if (!L.ok() || !c.begin(st)) return FAILED;
+  PkSource src;
+  src.idx = pk_idx;
+  src.off = pk_off;
+  return pipeline_verdicts(c, *d, msgs, nullptr, reinterpret_cast<const g2a *>(sigs), src, nullptr,
+                           true, m, ident.data(), m, verdicts, st)
              ? GBLS_SUCCESS
              : FAILED;
 }

@@ -50,8 +50,12 @@ void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uin
 // empty_is_error, s has no sets; an empty segment's partial is the identity otherwise.
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
-                  const g1a *pks, const uint64_t *rands, const int32_t *pre, int empty_is_error,
-                  g2j *part, int32_t *part_err, g1a *P, g2a *H, int32_t *seg_err);
+                  const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
+                  int empty_is_error, g2j *part, int32_t *part_err, g1a *P, g2a *H,
+                  int32_t *seg_err);
+// single checks (r = 1, one set per segment): the extra pair of segment s is (-g1, sig_s)
+void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
+                     const int32_t *pre2, uint32_t n, g1a *P, g2a *H, int32_t *seg_err);
 
 // k_lines.hip -- Miller-loop line functions of every pair
 // lines of pairs [first, first + count) of np (H indexed by pair)

@@ -15,9 +15,12 @@ __global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t 
   uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
   g1a pk = pks[i];
-  uint64_t r = rands ? rands[i] : 1;
+  if (!rands) {  // r = 1 (single checks): the key itself
+    P[i] = pk;
+    return;
+  }
   g1j t;
-  mul_u64(t, pk, r);
+  mul_u64(t, pk, rands[i]);
   g1a o;
   jac_to_aff(o, t);
   P[i] = o;
@@ -73,8 +76,8 @@ __device__ void wg_reduce_jac(jac<F> &v) {
 // combination, so it fails closed), or a failed pre-check
 __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32_t *chunks, uint32_t n,
                                                       const g1a *pks, const uint64_t *rands,
-                                                      const int32_t *pre, g2j *part,
-                                                      int32_t *part_err) {
+                                                      const int32_t *pre, const int32_t *pre2,
+                                                      g2j *part, int32_t *part_err) {
   __shared__ int32_t e_sh;
   uint32_t c = blockIdx.x;
   uint32_t h = chunks[4 * c + 1], b = chunks[4 * c + 2], e = chunks[4 * c + 3];
@@ -87,7 +90,10 @@ __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32
     g2j r = R[(size_t)h * n + i];
     jac_add(acc, acc, r);
     if (h == 0)
-      bad |= (aff_is_inf(pks[i]) || (rands && rands[i] == 0) || (pre && pre[i] != 0)) ? 1 : 0;
+      bad |= (aff_is_inf(pks[i]) || (rands && rands[i] == 0) || (pre && pre[i] != 0) ||
+              (pre2 && pre2[i] != 0))
+                 ? 1
+                 : 0;
   }
   if (bad) atomicOr(&e_sh, 1);
   wg_reduce_jac(acc);
@@ -155,6 +161,26 @@ __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32
   seg_err[s] = err;
 }
 
+// Single checks (r_i = 1, one set per segment: verify / fast_aggregate_verify batches):
+// S_s = sig_s, so the segment's extra pair is (-g1, sig_s) -- no G2 sum, no inversion.
+__global__ void __launch_bounds__(WG) k_single_S(const g2a *sigs, const g1a *pks, const int32_t *pre,
+                                                 const int32_t *pre2, uint32_t n, g1a *P, g2a *H,
+                                                 int32_t *seg_err) {
+  uint32_t s = blockIdx.x * WG + threadIdx.x;
+  if (s >= n) return;
+  g1a ng1;
+  fp_set(ng1.x, k::G1X_M);
+  fp_set(ng1.y, k::G1NEGY_M);
+  P[n + s] = ng1;
+  H[n + s] = sigs[s];
+  seg_err[s] = (aff_is_inf(pks[s]) || (pre && pre[s] != 0) || (pre2 && pre2[s] != 0)) ? 1 : 0;
+}
+
+void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
+                     const int32_t *pre2, uint32_t n, g1a *P, g2a *H, int32_t *seg_err) {
+  if (n) k_single_S<<<nblk(n), WG, 0, st>>>(sigs, pks, pre, pre2, n, P, H, seg_err);
+}
+
 void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1a *P) {
   if (n) k_mv_g1mul<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
 }
@@ -163,9 +189,11 @@ void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uin
 }
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
-                  const g1a *pks, const uint64_t *rands, const int32_t *pre, int empty_is_error,
-                  g2j *part, int32_t *part_err, g1a *P, g2a *H, int32_t *seg_err) {
-  if (nchunks) k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, rands, pre, part, part_err);
+                  const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
+                  int empty_is_error, g2j *part, int32_t *part_err, g1a *P, g2a *H,
+                  int32_t *seg_err) {
+  if (nchunks)
+    k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, rands, pre, pre2, part, part_err);
   if (nseg)
     k_g2sum_final<<<nseg, WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n,
                                        empty_is_error, P, H, seg_err);

@@ -59,6 +59,9 @@
  *   - Segment offsets must satisfy seg_off[0] == 0, seg_off[i] <= seg_off[i+1] and
  *     seg_off[nseg] == n (else GBLS_ERR_ARG).
  *   - A zero random scalar fails its batch (the reference only draws NonZeroU64).
+ *   - Concurrent host-pointer multi_verify calls (gbls_multi_verify, _segments,
+ *     _indexed) are coalesced: callers that arrive while the engine is busy are merged
+ *     into one segmented submission, each keeping its own verdicts.
  *   - There is NO CPU fallback inside this library: without a usable gfx950 device
  *     every call fails with GBLS_ERR_NO_DEVICE.
  */
@@ -100,6 +103,9 @@ enum {
   GBLS_ERR_ARG = 102,
 };
 
+/* gbls_init flags: low byte = engines per device; GBLS_INIT_NO_COALESCE turns off the
+ * cross-caller coalescing of concurrent host-pointer multi_verify calls (f3). */
+#define GBLS_INIT_NO_COALESCE 0x100u
 int gbls_init(uint32_t device_mask, uint32_t flags);
 int gbls_last_error(void);
 const char *gbls_version(void);
