@@ -131,6 +131,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "C5"])
     ap.add_argument("--sets", type=int, default=0, help="override the per-config batch size")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="batches in flight per GPU: step k runs on stream k %% inflight (1 GPU only)")
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's host CPU share")
     ap.add_argument("--no-cpu", action="store_true")
@@ -211,7 +213,8 @@ def main():
         d_rands = torch.tensor(to_i64(rands), dtype=torch.int64, device=dev)
         d_idx = dnp(idx) if idx is not None else None
         d_off = dnp(off) if off is not None else None
-        d_verdict = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        d_verdicts = [torch.full((1,), -1, dtype=torch.int32, device=dev) for _ in range(max(1, args.inflight))]
+        d_verdict = d_verdicts[0]
         d_part = torch.zeros(576, dtype=torch.uint8, device=dev)
         d_err = torch.zeros(1, dtype=torch.int32, device=dev)
         d_parts = torch.zeros(world * 576, dtype=torch.uint8, device=dev)
@@ -219,17 +222,18 @@ def main():
         seg = G.u32_array([0, n])
         leg.units = n
 
-        def step():
+        def step(slot=0):
             st = cur_stream()
             pidx = ptr(d_idx) if d_idx is not None else None
             poff = ptr(d_off) if d_off is not None else None
             if world == 1:
+                v = d_verdicts[slot]
                 if cfg == "C2":
                     rc = L.gbls_multi_verify_segments_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n,
-                                                             seg, 1, ptr(d_verdict), st)
+                                                             seg, 1, ptr(v), st)
                 else:
                     rc = L.gbls_multi_verify_indexed_segments_device(ptr(d_msgs), ptr(d_sigs), pidx, poff,
-                                                                     ptr(d_rands), n, seg, 1, ptr(d_verdict), st)
+                                                                     ptr(d_rands), n, seg, 1, ptr(v), st)
                 G.check(rc, "multi_verify device")
                 return
             if cfg == "C2":
@@ -246,7 +250,7 @@ def main():
             G.check(rc, "final_verify_partials")
 
         def verdict_ok():
-            return int(d_verdict.item()) == G.SUCCESS
+            return all(int(v.item()) == G.SUCCESS for v in (d_verdicts if world == 1 else [d_verdict]))
 
         leg.stage_units = lambda s: {"k_ml_leaf": n + 1, "k_ml_reduce": n + 1, "k_lines_S": 1,
                                      "k_g1_aggregate_idx": getattr(leg, "pks_per_step", n)}.get(s, n)
@@ -277,7 +281,7 @@ def main():
         leg.workload = ("C3: %d messages per GPU, each fast_aggregate_verify against the same %d-key sync "
                         "committee (registry indices, aggregated on device every step), 1%% invalid" % (m, k))
 
-        def step():
+        def step(slot=0):
             G.check(L.gbls_fast_aggregate_verify_indexed_device(ptr(d_sigs), ptr(d_msgs), ptr(d_idx), ptr(d_off), m,
                                                                 ptr(d_v), cur_stream()), "fav indexed device")
 
@@ -290,8 +294,20 @@ def main():
     else:
         return bench_c1(args, L, G, F, np)
 
-    for _ in range(args.warmup):
-        step()
+    D = max(1, args.inflight) if world == 1 and cfg != "C3" else 1
+    streams = [torch.cuda.Stream() for _ in range(D)] if D > 1 else None
+
+    def run(k):
+        if streams is None:
+            step()
+            return
+        s = streams[k % D]
+        s.wait_stream(torch.cuda.default_stream()) if k < D else None
+        with torch.cuda.stream(s):
+            step(k % D)
+
+    for k in range(max(args.warmup, D)):
+        run(k)
     torch.cuda.synchronize()
     if not verdict_ok():
         raise SystemExit("verdicts of the warm-up step are WRONG")
@@ -302,8 +318,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        run(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -352,6 +368,7 @@ def main():
                 "scaling": leg.scaling, "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
                 "data": "synthetic (seeded keys, messages and scalars; signed on device)",
                 "config": {"workload": leg.workload, "config": cfg, "units_per_gpu_per_step": leg.units,
+                           "batches_in_flight": D,
                            "parallelism": "shard sets, RCCL all-gather of Fp12 partials" if world > 1 else "1 GPU"},
                 "roofline": roof, "cpu_baseline": cpu}
         if cfg in ("C2", "C4", "C5"):

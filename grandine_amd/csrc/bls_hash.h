@@ -215,6 +215,45 @@ HD void fp_from_be64_words(fp &r, const uint32_t *w) {
 }
 
 // ---------------------------------------------------------------- SSWU + isogeny
+// fp2_sqrt_given_norm_root (bls_field.h) that also returns 1/nd for an nd != 0 in Fp,
+// without an inversion: the exponentiation runs on delta nd^4 instead of delta,
+//   t' = (delta nd^4)^((p-3)/4) = t nd^(p-3) = t / nd^2     (t = delta^((p-3)/4))
+// so t = t' nd^2, chi = delta t^2 = +-1 (delta's quadratic character), 1/t = chi delta t
+// and 1/nd = nd (t' / t) = chi nd t' t delta.  delta = 0 (only when a = 0) has no
+// character; that case falls back to the binary-GCD inversion.
+HD void fp2_sqrt_norm_inv(fp2 &r, fp &ndinv, const fp2 &a, const fp &gamma, const fp &nd) {
+  fp delta, t, tp, x0, x0sq, tmp, nd2, u;
+  fp_add(delta, a.c0, gamma);
+  fp_half(delta, delta);
+  if (fp_is_zero(delta)) {  // only when a1 == 0 and gamma == -a0
+    fp_sub(delta, a.c0, gamma);
+    fp_half(delta, delta);
+  }
+  fp_sqr(nd2, nd);
+  fp_sqr(u, nd2);
+  fp_mul(u, u, delta);     // delta nd^4
+  fp_pow_pm3d4(tp, u);     // t'
+  fp_mul(t, tp, nd2);      // t
+  fp_mul(x0, delta, t);
+  fp_sqr(x0sq, x0);
+  fp half_a1t;
+  fp_mul(tmp, a.c1, t);
+  fp_half(half_a1t, tmp);
+  bool sq = fp_eq(x0sq, delta);  // chi = +1
+  fp nh;
+  fp_neg(nh, half_a1t);
+  fp_sel(r.c0, sq, nh, x0);
+  fp_sel(r.c1, sq, x0, half_a1t);
+  if (fp_is_zero(delta)) {
+    fp_inv(ndinv, nd);
+    return;
+  }
+  fp_mul(u, nd, tp);
+  fp_mul(u, u, x0);        // nd t' t delta
+  fp_neg(tmp, u);
+  fp_sel(ndinv, sq, tmp, u);
+}
+
 // Simplified SWU on E2': y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2), inversion-free up to
 // one final Fp2 inversion, returning a Jacobian point on E2'.
 HD void map_to_curve_sswu(g2j &out, const fp2 &u) {
@@ -276,10 +315,16 @@ HD void map_to_curve_sswu(g2j &out, const fp2 &u) {
   fp2 Nx2;
   fp2_mul(Nx2, zu2, N);
   fp2_sel(Nsel, is_sq, Nx2, N);
-  fp2_sqrt_given_norm_root(s, a, gsel);  // s^2 = U_sel D
-  // affine: x = Nsel / D, y = s / D^2  (sgn0 needs the affine y)
+  // s^2 = U_sel D, and 1/N(D) from the same exponentiation (fp2_sqrt_norm_inv)
+  fp nd, ndt, ndinv;
+  fp_sqr(nd, D.c0);
+  fp_sqr(ndt, D.c1);
+  fp_add(nd, nd, ndt);
+  fp2_sqrt_norm_inv(s, ndinv, a, gsel, nd);
+  // affine: x = Nsel / D, y = s / D^2  (sgn0 needs the affine y); 1/D = conj(D) / N(D)
   fp2 Di, Di2, x, y;
-  fp2_inv(Di, D);
+  fp2_conj(Di, D);
+  fp2_mul_fp(Di, Di, ndinv);
   fp2_sqr(Di2, Di);
   fp2_mul(x, Nsel, Di);
   fp2_mul(y, s, Di2);
