@@ -85,6 +85,18 @@ _sz = _c.c_size_t
 _vp = _c.c_void_p
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm bundles its own libamdhip64 with the same soname as /opt/rocm's.  The
+    first one loaded serves the whole process, and torch cannot enumerate devices on a
+    runtime other than its own -- so when torch is installed, load it before the engine
+    so both share torch's HIP runtime (the engine's device buffers are then ordinary
+    torch-visible allocations and streams interoperate)."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_library():
     """Load the shared library without touching the GPU (symbol checks only)."""
     global _lib
@@ -92,6 +104,7 @@ def load_library():
         if _lib is None:
             if not os.path.exists(LIB_PATH):
                 raise EngineUnavailable(f"{LIB_PATH} not built (run __graft_entry__.build())")
+            _share_torch_hip_runtime()
             lib = _c.CDLL(LIB_PATH)
             sig = {
                 "gbls_init": (_c.c_int, [_c.c_uint32, _c.c_uint32]),

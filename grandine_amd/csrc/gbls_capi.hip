@@ -23,6 +23,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -132,7 +133,7 @@ struct Ctx {
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
   Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, gpart, lines, V0, V1, tab, part, err, out0,
-      out1, pks, pre, pre2;
+      out1, pks, pre, pre2, msm;
   void *stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
   std::vector<uint32_t> host_tab;  // table assembly, reused across calls
@@ -239,6 +240,7 @@ struct Engine {
   std::shared_mutex reg_mu;
   size_t reg_n = 0;
   std::atomic<bool> coalesce{true};
+  size_t msm_min = 16384;  // single-segment batches at least this large use the bucket MSM
 } g;
 
 // RAII lease of a context of one device: the idle context last used on the caller's
@@ -316,6 +318,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
   }
   if (ids.empty()) return fail(GBLS_ERR_NO_DEVICE);
   g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
+  if (const char *e = std::getenv("GBLS_MSM_MIN")) g.msm_min = std::strtoull(e, nullptr, 10);
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
   for (int id : ids) {
@@ -403,6 +406,12 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   const size_t np = n + nseg;
   bool single = !rands && n == nseg;  // one set per segment, r = 1
   for (size_t s = 0; single && s <= nseg; s++) single = seg_off[s] == s;
+  const bool msm = rands && nseg == 1 && n >= g.msm_min;  // bucket MSM for S
+  MsmPlan mp{};
+  if (msm) {
+    mp = msm_plan((uint32_t)n);
+    if (!c.ensure(c.msm, mp.bytes)) return false;
+  }
   // ---- host tables, one staged upload:
   //   [couples][g2 chunks][seg_chunk][reduction levels][seg_off]
   std::vector<uint32_t> &tab = c.host_tab;
@@ -501,14 +510,19 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     launch_g2_check(c.side2, sigs, N, c.pre2.as<int32_t>(), 0);
     pre2 = c.pre2.as<int32_t>();
   }
-  if (!single) {
+  if (msm) {
+    StageTimer t(S_G2MUL, c.side2);
+    launch_msm(c.side2, mp, c.msm.as<uint8_t>(), sigs, rands, N, c.H.as<g2a>(), c.P.as<g1a>());
+  } else if (!single) {
     StageTimer t(S_G2MUL, c.side2);
     launch_mv_g2mul(c.side2, sigs, rands, N, c.R.as<g2j>());
   }
   HIPCHK(hipStreamWaitEvent(c.side2, c.ev_pks, 0));
   {
     StageTimer t(S_G2SUM, c.side2);
-    if (single)
+    if (msm)
+      launch_msm_flags(c.side2, pks, rands, pre, pre2, N, seg_err);
+    else if (single)
       launch_single_S(c.side2, sigs, pks, pre, pre2, N, c.P.as<g1a>(), c.H.as<g2a>(), seg_err);
     else
       launch_g2sum(c.side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,

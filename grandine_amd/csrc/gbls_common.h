@@ -57,6 +57,20 @@ void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t
 void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
                      const int32_t *pre2, uint32_t n, g1a *P, g2a *H, int32_t *seg_err);
 
+// k_msm.hip -- S = sum r_i sig_i of one large segment by a signed-digit bucket MSM
+struct MsmPlan {
+  int c, W;             // window bits, windows
+  uint32_t nb;          // buckets (W * 2^(c-1))
+  uint32_t max_chunks;  // bound on the chunk count (grid of the chunk kernel)
+  size_t o_cnt, o_start, o_cur, o_cstart, o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
+};
+MsmPlan msm_plan(uint32_t n);
+// writes the segment's extra pair (P[n] = -g1, H[n] = affine S)
+void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
+                const uint64_t *rands, uint32_t n, g2a *H, g1a *P);
+void launch_msm_flags(hipStream_t st, const g1a *pks, const uint64_t *rands, const int32_t *pre,
+                      const int32_t *pre2, uint32_t n, int32_t *seg_err);
+
 // k_lines.hip -- Miller-loop line functions of every pair
 // lines of pairs [first, first + count) of np (H indexed by pair)
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,

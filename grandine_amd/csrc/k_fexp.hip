@@ -13,10 +13,12 @@ __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const in
   W12_SHARED uint32_t f[W12_WORDS], F[W12_WORDS], A[W12_WORDS], B[W12_WORDS], T[W12_WORDS],
       X[W12_WORDS], ws[W12_WS_WORDS];
   __shared__ int bad;
+  int lane = threadIdx.x;
   w12_plan pl;
   w12_begin(pl, ws);
+  w12_cplan cp;
+  w12_cplan_load(cp, lane);
   uint32_t s = blockIdx.x;
-  int lane = threadIdx.x;
   const uint32_t *src = reinterpret_cast<const uint32_t *>(part + s);
   for (int i = lane; i < W12_WORDS; i += 64) f[i] = src[i];
   if (lane == 0) bad = err[s];
@@ -35,19 +37,19 @@ __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const in
   w12_frob2(F, A);
   w12_mul(pl, F, F, A, ws);
   // A = F^(x-1) = F^x conj(F);  A = A^(x-1)
-  w12_cyc_exp_x(pl, A, F, ws);
+  w12_cyc_exp_x(pl, cp, A, F, ws);
   w12_conj(X, F);
   w12_mul(pl, A, A, X, ws);
-  w12_cyc_exp_x(pl, B, A, ws);
+  w12_cyc_exp_x(pl, cp, B, A, ws);
   w12_conj(X, A);
   w12_mul(pl, A, B, X, ws);
   // B = A^(x+p) = A^x frob(A)
-  w12_cyc_exp_x(pl, B, A, ws);
+  w12_cyc_exp_x(pl, cp, B, A, ws);
   w12_frob(X, A);
   w12_mul(pl, B, B, X, ws);
   // T = B^x;  C = T^x frob2(B) conj(B)   (C in A)
-  w12_cyc_exp_x(pl, T, B, ws);
-  w12_cyc_exp_x(pl, A, T, ws);
+  w12_cyc_exp_x(pl, cp, T, B, ws);
+  w12_cyc_exp_x(pl, cp, A, T, ws);
   w12_frob2(X, B);
   w12_mul(pl, A, A, X, ws);
   w12_conj(X, B);

@@ -145,10 +145,25 @@ static void w12_mul_host(uint32_t *c, const uint32_t *a, const uint32_t *b) {
 static void w12_conj_host(uint32_t *c, const uint32_t *a) {
   for (int l = 0; l < 64; l++) w12_r_conj(l, a, c);
 }
+static void w12_cyc_sqr_host(uint32_t *c, const uint32_t *a) {
+  static uint32_t ws[W12_WS_WORDS];
+  static w12_cplan cp[64];
+  static bool init = false;
+  if (!init) {
+    for (int l = 0; l < 64; l++) {
+      w12_cplan_load(cp[l], l);
+      w12_r_ws_init(l, ws);
+    }
+    init = true;
+  }
+  for (int l = 0; l < 64; l++) w12_r_cmul(l, cp[l], a, ws);
+  for (int l = 0; l < 64; l++) w12_r_cpost1(l, cp[l], ws);
+  for (int l = 0; l < 64; l++) w12_r_cpost2(l, cp[l], a, ws, c);
+}
 static void w12_exp_x_host(uint32_t *c, const uint32_t *a) {
   for (int l = 0; l < 64; l++) w12_r_copy(l, a, c);
   for (int i = 62; i >= 0; i--) {
-    w12_mul_host(c, c, c);
+    w12_cyc_sqr_host(c, c);
     if ((k::X_ABS >> i) & 1) w12_mul_host(c, c, a);
   }
   w12_conj_host(c, c);
@@ -181,6 +196,25 @@ static bool w12_final_exp_is_one_host(const fp12 &f0) {
   w12_mul_host(X, X, F);
   w12_mul_host(A, A, X);
   return w12_is_one_image(A);
+}
+
+// cyclotomic squaring of the wave engine vs the generic Fp12 squaring, on the easy-part
+// image F = (conj(f) / f)^(p^2 + 1) of an arbitrary f (F is in the cyclotomic subgroup)
+int h_w12_cyc_sqr_check(const uint8_t *f576) {
+  fp12 f, t0, t1, F, ref;
+  std::memcpy(&f, f576, 576);
+  fp12_inv(t0, f);
+  fp12_conj(t1, f);
+  fp12_mul(t1, t1, t0);
+  fp12_frob2(t0, t1);
+  fp12_mul(F, t0, t1);
+  fp12_sqr(ref, F);
+  uint32_t a[144], c[144];
+  std::memcpy(a, &F, 576);
+  w12_cyc_sqr_host(c, a);
+  int ok = std::memcmp(c, &ref, 576) == 0;
+  w12_cyc_sqr_host(a, a);  // in place
+  return ok && std::memcmp(a, &ref, 576) == 0;
 }
 
 void h_fp12_mul_w12(const uint8_t *a576, const uint8_t *b576, uint8_t *out576) {

@@ -266,6 +266,22 @@ def test_multi_engine_sharding_subprocess():
                    "registry": 0}
 
 
+def test_bucket_msm_parity_subprocess():
+    """n1: the bucket-MSM path for S (k_msm.hip), forced on every batch size
+    (GBLS_MSM_MIN=1): golden multi_verify verdicts, and 4096-set batches (valid, swapped
+    signature, infinite signature, crowded and near-empty buckets) equal to the C
+    oracle's verdicts; a zero scalar fails closed."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_msm.py")], capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert all(res["golden"]), res
+    for name, gpu, ref in res["c2"]:
+        assert gpu == ref, (name, gpu, ref)
+    assert [x[1] for x in res["c2"]] == [True, False, False, True, True]
+    assert res["zero_scalar"] == 5
+
+
 # ------------------------------------------------------------------ registry (C4 / C5 shapes)
 N_REG = 1_700_000
 

@@ -134,3 +134,13 @@ def test_multi_verify_fixtures(H):
         rands = (ctypes.c_uint64 * n)(*[int(r) for r in c["rands"]])
         msgs = b"".join(bytes.fromhex(h) for h in c["msgs"])
         assert (H.h_multi_verify(msgs, sigs, pks, rands, n) == 0) == c["expect"], c["note"]
+
+
+def test_w12_cyclotomic_squaring_matches_generic(H):
+    """The wave engine's Granger-Scott squaring (final exponentiation hard part) equals
+    the generic Fp12 squaring on cyclotomic-subgroup elements, out of place and in place."""
+    import random
+    rng = random.Random(7)
+    for _ in range(20):
+        f = b"".join(fp_b(rng.randrange(O.P)) for _ in range(12))
+        assert H.h_w12_cyc_sqr_check(f) == 1
