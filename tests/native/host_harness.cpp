@@ -145,40 +145,23 @@ static void w12_mul_host(uint32_t *c, const uint32_t *a, const uint32_t *b) {
 static void w12_conj_host(uint32_t *c, const uint32_t *a) {
   for (int l = 0; l < 64; l++) w12_r_conj(l, a, c);
 }
-static void w12_cyc_sqr_host(uint32_t *c, const uint32_t *a) {
-  static uint32_t ws[W12_WS_WORDS];
-  static w12_cplan cp[64];
-  static bool init = false;
-  if (!init) {
-    for (int l = 0; l < 64; l++) {
-      w12_cplan_load(cp[l], l);
-      w12_r_ws_init(l, ws);
-    }
-    init = true;
-  }
-  for (int l = 0; l < 64; l++) w12_r_cmul(l, cp[l], a, ws);
-  for (int l = 0; l < 64; l++) w12_r_cpost1(l, cp[l], ws);
-  for (int l = 0; l < 64; l++) w12_r_cpost2(l, cp[l], a, ws, c);
-}
 static void w12_exp_x_host(uint32_t *c, const uint32_t *a) {
   for (int l = 0; l < 64; l++) w12_r_copy(l, a, c);
   for (int i = 62; i >= 0; i--) {
-    w12_cyc_sqr_host(c, c);
+    w12_mul_host(c, c, c);
     if ((k::X_ABS >> i) & 1) w12_mul_host(c, c, a);
   }
   w12_conj_host(c, c);
 }
-// k_final_verdict's chain on the host engine emulation
-static bool w12_final_exp_is_one_host(const fp12 &f0) {
-  uint32_t f[144], F[144], A[144], B[144], T[144], X[144];
+// k_final_verdict's inversion-free chain on the host engine emulation
+static bool w12_final_verdict_host(const fp12 &f0) {
+  uint32_t f[144], G[144], A[144], B[144], T[144], X[144];
   std::memcpy(f, &f0, sizeof f);
-  for (int l = 0; l < 64; l++) w12_r_inv(l, f, X);
-  w12_conj_host(A, f);
-  w12_mul_host(A, A, X);
-  for (int l = 0; l < 64; l++) w12_r_frob2(l, A, F);
-  w12_mul_host(F, F, A);
-  w12_exp_x_host(A, F);
-  w12_conj_host(X, F);
+  if (w12_is_zero_image(f)) return false;
+  for (int l = 0; l < 64; l++) w12_r_frob2(l, f, G);
+  w12_mul_host(G, G, f);
+  w12_exp_x_host(A, G);
+  w12_conj_host(X, G);
   w12_mul_host(A, A, X);
   w12_exp_x_host(B, A);
   w12_conj_host(X, A);
@@ -192,29 +175,30 @@ static bool w12_final_exp_is_one_host(const fp12 &f0) {
   w12_mul_host(A, A, X);
   w12_conj_host(X, B);
   w12_mul_host(A, A, X);
-  w12_mul_host(X, F, F);
-  w12_mul_host(X, X, F);
+  w12_mul_host(X, G, G);
+  w12_mul_host(X, X, G);
   w12_mul_host(A, A, X);
-  return w12_is_one_image(A);
+  return w12_is_fp6_image(A);
 }
-
-// cyclotomic squaring of the wave engine vs the generic Fp12 squaring, on the easy-part
-// image F = (conj(f) / f)^(p^2 + 1) of an arbitrary f (F is in the cyclotomic subgroup)
-int h_w12_cyc_sqr_check(const uint8_t *f576) {
-  fp12 f, t0, t1, F, ref;
+// the device verdict and the textbook final exponentiation (bls_pairing.h) on one value
+int h_w12_verdict(const uint8_t *f576) {
+  fp12 f;
   std::memcpy(&f, f576, 576);
-  fp12_inv(t0, f);
-  fp12_conj(t1, f);
-  fp12_mul(t1, t1, t0);
-  fp12_frob2(t0, t1);
-  fp12_mul(F, t0, t1);
-  fp12_sqr(ref, F);
-  uint32_t a[144], c[144];
-  std::memcpy(a, &F, 576);
-  w12_cyc_sqr_host(c, a);
-  int ok = std::memcmp(c, &ref, 576) == 0;
-  w12_cyc_sqr_host(a, a);  // in place
-  return ok && std::memcmp(a, &ref, 576) == 0;
+  return w12_final_verdict_host(f);
+}
+int h_final_exp_is_one(const uint8_t *f576) {
+  fp12 f, r;
+  std::memcpy(&f, f576, 576);
+  final_exp(r, f);
+  return fp12_is_one(r);
+}
+// Miller partial of a multi_verify batch on the host (the device pipeline's formulas)
+void h_fp12_mul(const uint8_t *a576, const uint8_t *b576, uint8_t *out576) {
+  fp12 a, b, r;
+  std::memcpy(&a, a576, 576);
+  std::memcpy(&b, b576, 576);
+  fp12_mul(r, a, b);
+  std::memcpy(out576, &r, 576);
 }
 
 void h_fp12_mul_w12(const uint8_t *a576, const uint8_t *b576, uint8_t *out576) {
@@ -306,7 +290,7 @@ static void pipeline(const uint8_t *msgs, const uint32_t *msg_off, const uint8_t
       }
     }
     fp12_conj(f, f);
-    verdicts[s] = (!err && w12_final_exp_is_one_host(f)) ? ST_SUCCESS : ST_VERIFY_FAIL;
+    verdicts[s] = (!err && w12_final_verdict_host(f)) ? ST_SUCCESS : ST_VERIFY_FAIL;
   }
 }
 

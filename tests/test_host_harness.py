@@ -136,11 +136,34 @@ def test_multi_verify_fixtures(H):
         assert (H.h_multi_verify(msgs, sigs, pks, rands, n) == 0) == c["expect"], c["note"]
 
 
-def test_w12_cyclotomic_squaring_matches_generic(H):
-    """The wave engine's Granger-Scott squaring (final exponentiation hard part) equals
-    the generic Fp12 squaring on cyclotomic-subgroup elements, out of place and in place."""
+def test_inversion_free_final_verdict(H):
+    """k_final_verdict's test "Psi(f^(p^2+1)) has zero w-half" equals the textbook
+    "final_exp(f) == 1": on a valid batch's Miller product (true), on that product times
+    Fp6 elements (killed by the p^6 - 1 of the final exponentiation: still true), and on
+    products times elements outside Fp6 (false)."""
     import random
-    rng = random.Random(7)
-    for _ in range(20):
-        f = b"".join(fp_b(rng.randrange(O.P)) for _ in range(12))
-        assert H.h_w12_cyc_sqr_check(f) == 1
+    rng = random.Random(11)
+    C = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libbls_ref.so"))
+    C.ref_multi_verify_partial.argtypes = [ctypes.c_char_p] * 3 + [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
+                                                                   ctypes.c_char_p]
+    cases = gold("multi_verify")["cases"]
+    c = next(x for x in cases if x["expect"] and len(x["msgs"]) >= 6)
+    msgs = b"".join(bytes.fromhex(h) for h in c["msgs"])
+    sigs = b"".join(g2_b(O.g2_decompress(bytes.fromhex(h))[1]) for h in c["sigs"])
+    pks = b"".join(g1_b(O.g1_decompress(bytes.fromhex(h))[1]) for h in c["pks"])
+    n = len(c["msgs"])
+    part = ctypes.create_string_buffer(576)
+    assert C.ref_multi_verify_partial(msgs, sigs, pks, (ctypes.c_uint64 * n)(*[int(r) for r in c["rands"]]), n,
+                                      part) == 0
+    f = part.raw
+    assert H.h_final_exp_is_one(f) == 1 and H.h_w12_verdict(f) == 1
+    out = ctypes.create_string_buffer(576)
+    for trial in range(6):
+        coefs = [rng.randrange(O.P) for _ in range(12)]
+        if trial < 3:
+            coefs[6:] = [0] * 6  # an Fp6 element
+        H.h_fp12_mul(f, b"".join(fp_b(x) for x in coefs), out)
+        want = H.h_final_exp_is_one(out.raw)
+        assert want == (trial < 3)
+        assert H.h_w12_verdict(out.raw) == want
+    assert H.h_w12_verdict(bytes(576)) == 0

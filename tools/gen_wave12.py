@@ -174,98 +174,7 @@ def main():
         w("  {%s}," % ", ".join("0x%08xu" % x for x in words))
     w("};")
     w("}}  // namespace gbls::w12")
-    out += cyclotomic_square_plan()
     print("\n".join(out))
-
-
-def cyclotomic_square_plan():
-    """Plan of the wave-cooperative cyclotomic squaring (Granger-Scott), valid for f in
-    the cyclotomic subgroup (after the easy part of the final exponentiation).
-
-    With g0..g5 the Fp2 coefficients of f = sum g_i w^i (g0 = c0.c0, g1 = c1.c0,
-    g2 = c0.c1, g3 = c1.c1, g4 = c0.c2, g5 = c1.c2) and s = w^3 (s^2 = xi), f = A + B w
-    + C w^2 over Fp4 = Fp2[s] with A = g0 + g3 s, B = g1 + g4 s, C = g2 + g5 s, and
-        f^2 = (3 A^2 - 2 conj(A)) + (3 s C^2 + 2 conj(B)) w + (3 B^2 - 2 conj(C)) w^2.
-    MUL   lane l < 27: one Fp product; per Fp4 square (X, Y): x0^2, x1^2, x0 x1, y0^2,
-          y1^2, y0 y1, (x0+y0)^2, (x1+y1)^2, (x0+y0)(x1+y1)
-    POST1 lane l < 12: (X + Y s)^2 = c0 + c1 s, c0 = X^2 + xi Y^2, c1 = 2XY, as signed
-          sums of products (<= 5 positive + 4 negative)
-    POST2 lane l < 12: output coefficient 3 u + 2 g or 3 u - 2 g, u = one POST1 value or
-          (xi c1)'s component t_a -+ t_b.
-    """
-    def idx(h, j, k):
-        return h * 6 + j * 2 + k
-    g = [(0, 0), (1, 0), (0, 1), (1, 1), (0, 2), (1, 2)]  # g_i -> (h, j)
-
-    def coef(i, k):
-        return idx(g[i][0], g[i][1], k)
-    NONE = 12
-    squares = [(0, 3), (1, 4), (2, 5)]  # A, B, C
-    mul = []
-    for (a, b) in squares:
-        x0, x1, y0, y1 = coef(a, 0), coef(a, 1), coef(b, 0), coef(b, 1)
-        mul += [((x0, NONE), (x0, NONE)), ((x1, NONE), (x1, NONE)), ((x0, NONE), (x1, NONE)),
-                ((y0, NONE), (y0, NONE)), ((y1, NONE), (y1, NONE)), ((y0, NONE), (y1, NONE)),
-                ((x0, y0), (x0, y0)), ((x1, y1), (x1, y1)), ((x0, y0), (x1, y1))]
-    assert len(mul) == 27
-    post1 = []  # per square: c0r, c0i, c1r, c1i as (pos list, neg list) of product slots
-    for q in range(3):
-        P = [9 * q + t for t in range(9)]
-        post1.append(([P[0], P[3]], [P[1], P[4], P[5], P[5]]))
-        post1.append(([P[2], P[2], P[3], P[5], P[5]], [P[4]]))
-        post1.append(([P[6], P[1], P[4]], [P[7], P[0], P[3]]))
-        post1.append(([P[8], P[8]], [P[2], P[2], P[5], P[5]]))
-    NP1 = max(len(p) for p, _ in post1)
-    NN1 = max(len(n) for _, n in post1)
-    assert NP1 + NN1 <= 9
-    base1 = 27
-    zero = "ZERO"
-
-    def v1(q, t):  # POST1 value slot: square q, t in (c0r, c0i, c1r, c1i)
-        return base1 + 4 * q + t
-    # POST2: per output coefficient index o: (ta, tb, neg_b, g sign) -> 3 (ta +- tb) +- 2 a[o]
-    post2 = {}
-    for k in range(2):
-        post2[coef(0, k)] = (v1(0, k), None, 0, -1)       # g0' = 3 c0(A) - 2 g0
-        post2[coef(3, k)] = (v1(0, 2 + k), None, 0, +1)   # g3' = 3 c1(A) + 2 g3
-        post2[coef(2, k)] = (v1(1, k), None, 0, -1)       # g2' = 3 c0(B) - 2 g2
-        post2[coef(5, k)] = (v1(1, 2 + k), None, 0, +1)   # g5' = 3 c1(B) + 2 g5
-        post2[coef(4, k)] = (v1(2, k), None, 0, -1)       # g4' = 3 c0(C) - 2 g4
-    post2[coef(1, 0)] = (v1(2, 2), v1(2, 3), 1, +1)       # g1' = 3 xi c1(C) + 2 g1
-    post2[coef(1, 1)] = (v1(2, 2), v1(2, 3), 0, +1)
-    assert sorted(post2) == list(range(12))
-    lines = []
-    w = lines.append
-    w("// Cyclotomic squaring plan (tools/gen_wave12.py cyclotomic_square_plan): per lane")
-    w("// word 0: MUL operand bytes {x_a, x_b, y_a, y_b} (12 = none); words 1-3: POST1 bytes,")
-    w("// %d positive then %d negative value slots; word 3 byte 3 / word 4: POST2" % (NP1, NN1))
-    w("// {ta, tb, flags (bit0: subtract tb, bit1: subtract 2g)} (0xff = zero slot).")
-    w("namespace gbls { namespace w12 {")
-    w("constexpr int CYC_NMUL = 27, CYC_NPOST = 12, CYC_BASE1 = %d, CYC_NPOS1 = %d, CYC_NNEG1 = %d;"
-      % (base1, NP1, NN1))
-    w("GBLS_CONSTANT uint32_t CYC_PLAN[64][5] = {")
-    for l in range(64):
-        b = [0] * 20
-        if l < 27:
-            (xa, xb), (ya, yb) = mul[l]
-            b[0:4] = [xa, xb, ya, yb]
-        else:
-            b[0:4] = [NONE] * 4
-        if l < 12:
-            pos, neg = post1[l]
-            pos = pos + [0xff] * (NP1 - len(pos))
-            neg = neg + [0xff] * (NN1 - len(neg))
-            b[4:4 + NP1 + NN1] = pos + neg
-            ta, tb, nb, gs = post2[l]
-            b[16:19] = [ta, 0xff if tb is None else tb, (1 if nb else 0) | (2 if gs < 0 else 0)]
-        else:
-            b[4:4 + NP1 + NN1] = [0xff] * (NP1 + NN1)
-            b[16:19] = [0xff, 0xff, 0]
-        words = [sum(b[4 * i + j] << (8 * j) for j in range(4)) for i in range(5)]
-        w("  {%s}," % ", ".join("0x%08xu" % x for x in words))
-    w("};")
-    w("}}  // namespace gbls::w12")
-    return lines
 
 
 if __name__ == "__main__":
