@@ -1,15 +1,19 @@
 #!/usr/bin/env python3
 """Headline benchmark: verified BLS signature sets/s on MI355X (BASELINE.json metric).
 
-Default workload (BASELINE.json configs[1], SURVEY.md 8(d) "C2"): per rank, a synthetic
-batch of 4096 single-pubkey signature sets -- seeded secret keys, distinct 32-byte signing
-roots, sig_i = sk_i * H(m_i), nonzero 64-bit random scalars r_i -- verified by ONE
+Default workload (BASELINE.json configs[1], SURVEY.md 8(d) "C2"): synthetic batches of
+4096 single-pubkey signature sets -- seeded secret keys, distinct 32-byte signing roots,
+sig_i = sk_i * H(m_i), nonzero 64-bit random scalars r_i -- each verified by ONE
 random-linear-combination batch check, exactly Signature::multi_verify (reference
 bls/src/signature.rs:95-129, reached from MultiVerifier::finish,
-helper_functions/src/verifier.rs:301-323).  A "step" = one multi_verify of the batch,
-inputs already resident in HBM (decompressed points, as blst takes them); hash_to_G2 of
-every message, both scalar sides, the Miller product and the final exponentiation all
-run inside the timed region.
+helper_functions/src/verifier.rs:301-323).  A "step" = --batches (default 4) such
+batches in flight on one GPU, submitted together as segments of one device call the way
+the engine's cross-caller coalescer merges concurrent MultiVerifier::finish calls: every
+batch keeps its own scalars, its own S = sum r_i sig_i, its own final exponentiation and
+its own verdict.  Inputs are resident in HBM (decompressed points, as blst takes them);
+hash_to_G2 of every message, both scalar sides, the Miller products and the final
+exponentiations all run inside the timed region.  The same run also times ONE batch per
+step ("single_batch": the 4096-set latency view).
 
 Other legs (--config): C3 sync-committee fast_aggregate_verify (10,000 messages x 512
 registry keys; unit = messages), C4 an epoch of attestations (2,048 committees over a
@@ -133,6 +137,10 @@ def main():
     ap.add_argument("--sets", type=int, default=0, help="override the per-config batch size")
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight per GPU: step k runs on stream k %% inflight (1 GPU only)")
+    ap.add_argument("--batches", type=int, default=4,
+                    help="C2: independent batches per step, verified as segments of ONE device submission "
+                         "(each its own random linear combination, final exponentiation and verdict), as "
+                         "the engine's coalescer merges concurrent callers")
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's host CPU share")
     ap.add_argument("--no-cpu", action="store_true")
@@ -173,12 +181,21 @@ def main():
     cfg = args.config
     # ------------------------------------------------------------------ batch-verify legs
     if cfg in ("C2", "C4", "C5"):
+        nb = 1
         if cfg == "C2":
-            n = args.sets or 4096
-            msgs, sigs, pks, rands = F.c2_batch(n, seed=rank + 1)
+            per = args.sets or 4096
+            nb = max(1, args.batches)
+            parts = [F.c2_batch(per, seed=rank * 1000 + b + 1) for b in range(nb)]
+            msgs = b"".join(p[0] for p in parts)
+            sigs = b"".join(p[1] for p in parts)
+            pks = b"".join(p[2] for p in parts)
+            rands = [r for p in parts for r in p[3]]
+            n = per * nb
             d_pks = dbytes(pks)
             idx = off = None
-            leg.workload = "C2: %d single-pubkey sets per GPU, random-scalar multi_verify" % n
+            leg.workload = ("C2: %d single-pubkey sets per GPU, random-scalar multi_verify" % per if nb == 1 else
+                            "C2: %d independent batches of %d single-pubkey sets per GPU per step, each its own "
+                            "random-scalar multi_verify (segments of one submission)" % (nb, per))
         elif cfg == "C4":
             ncom = args.sets or 2048
             nreg = 1 << 20
@@ -213,14 +230,15 @@ def main():
         d_rands = torch.tensor(to_i64(rands), dtype=torch.int64, device=dev)
         d_idx = dnp(idx) if idx is not None else None
         d_off = dnp(off) if off is not None else None
-        d_verdicts = [torch.full((1,), -1, dtype=torch.int32, device=dev) for _ in range(max(1, args.inflight))]
+        d_verdicts = [torch.full((nb,), -1, dtype=torch.int32, device=dev) for _ in range(max(1, args.inflight))]
         d_verdict = d_verdicts[0]
-        d_part = torch.zeros(576, dtype=torch.uint8, device=dev)
-        d_err = torch.zeros(1, dtype=torch.int32, device=dev)
-        d_parts = torch.zeros(world * 576, dtype=torch.uint8, device=dev)
-        d_errs = torch.zeros(world, dtype=torch.int32, device=dev)
-        seg = G.u32_array([0, n])
+        d_part = torch.zeros(nb * 576, dtype=torch.uint8, device=dev)
+        d_err = torch.zeros(nb, dtype=torch.int32, device=dev)
+        d_parts = torch.zeros(world * nb * 576, dtype=torch.uint8, device=dev)
+        d_errs = torch.zeros(world * nb, dtype=torch.int32, device=dev)
+        seg = G.u32_array([n * b // nb for b in range(nb + 1)])
         leg.units = n
+        leg.segments = nb
 
         def step(slot=0):
             st = cur_stream()
@@ -230,7 +248,7 @@ def main():
                 v = d_verdicts[slot]
                 if cfg == "C2":
                     rc = L.gbls_multi_verify_segments_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n,
-                                                             seg, 1, ptr(v), st)
+                                                             seg, nb, ptr(v), st)
                 else:
                     rc = L.gbls_multi_verify_indexed_segments_device(ptr(d_msgs), ptr(d_sigs), pidx, poff,
                                                                      ptr(d_rands), n, seg, 1, ptr(v), st)
@@ -238,21 +256,21 @@ def main():
                 return
             if cfg == "C2":
                 rc = L.gbls_multi_verify_partials_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n, seg,
-                                                         1, ptr(d_part), ptr(d_err), st)
+                                                         nb, ptr(d_part), ptr(d_err), st)
             else:
                 rc = L.gbls_multi_verify_indexed_partials_device(ptr(d_msgs), ptr(d_sigs), pidx, poff, ptr(d_rands),
                                                                  n, seg, 1, ptr(d_part), ptr(d_err), st)
             G.check(rc, "multi_verify partials")
             dist.all_gather_into_tensor(d_parts, d_part)
             dist.all_gather_into_tensor(d_errs, d_err)
-            rc = L.gbls_final_verify_partials_device(ptr(d_parts), ptr(d_errs), world, 1, ptr(d_verdict),
+            rc = L.gbls_final_verify_partials_device(ptr(d_parts), ptr(d_errs), world, nb, ptr(d_verdict),
                                                      cur_stream())
             G.check(rc, "final_verify_partials")
 
         def verdict_ok():
-            return all(int(v.item()) == G.SUCCESS for v in (d_verdicts if world == 1 else [d_verdict]))
+            return all(bool((v == G.SUCCESS).all()) for v in (d_verdicts if world == 1 else [d_verdict]))
 
-        leg.stage_units = lambda s: {"k_ml_leaf": n + 1, "k_ml_reduce": n + 1, "k_lines_S": 1,
+        leg.stage_units = lambda s: {"k_ml_leaf": n + nb, "k_ml_reduce": n + nb, "k_lines_S": nb,
                                      "k_g1_aggregate_idx": getattr(leg, "pks_per_step", n)}.get(s, n)
     # ------------------------------------------------------------------ C3
     elif cfg == "C3":
@@ -336,6 +354,28 @@ def main():
     if not ok:
         raise SystemExit("verdicts changed during the timed region")
 
+    # ---- one batch per step (the 4096-set latency view), same inputs, after the main timing
+    single = None
+    if cfg == "C2" and world == 1 and leg.segments > 1:
+        per = leg.units // leg.segments
+        seg1 = G.u32_array([0, per])
+        v1 = torch.full((1,), -1, dtype=torch.int32, device=dev)
+
+        def step1():
+            G.check(L.gbls_multi_verify_segments_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), per,
+                                                        seg1, 1, ptr(v1), cur_stream()), "single batch")
+        step1()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step1()
+        torch.cuda.synchronize()
+        d1 = time.perf_counter() - t1
+        if int(v1.item()) != G.SUCCESS:
+            raise SystemExit("single-batch verdict WRONG")
+        single = {"batches_per_step": 1, "sets_per_step": per, "value": round(per * args.steps / d1, 1),
+                  "ms_per_step": round(d1 / args.steps * 1e3, 4)}
+
     # ---- roofline of the dominant kernel (HIP events on the launch stream)
     nst = 32
     ms = (ctypes.c_double * nst)()
@@ -368,11 +408,13 @@ def main():
                 "scaling": leg.scaling, "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
                 "data": "synthetic (seeded keys, messages and scalars; signed on device)",
                 "config": {"workload": leg.workload, "config": cfg, "units_per_gpu_per_step": leg.units,
-                           "batches_in_flight": D,
+                           "batches_per_step": getattr(leg, "segments", 1), "streams_in_flight": D,
                            "parallelism": "shard sets, RCCL all-gather of Fp12 partials" if world > 1 else "1 GPU"},
                 "roofline": roof, "cpu_baseline": cpu}
         if cfg in ("C2", "C4", "C5"):
-            line["pairings_per_s"] = round(world * (leg.units + 1) * args.steps / dt, 1)
+            line["pairings_per_s"] = round(world * (leg.units + leg.segments) * args.steps / dt, 1)
+        if single:
+            line["single_batch"] = single
         if cfg == "C4":
             line["pks_aggregated_per_s"] = round(world * leg.pks_per_step * args.steps / dt, 1)
         print(json.dumps(line), flush=True)
