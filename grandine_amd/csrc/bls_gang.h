@@ -180,6 +180,118 @@ __device__ __forceinline__ void gang_add(g2j &r, const g2j &a, const g2j &b, int
   fp2_sub(r.y, t, S1);        // Y3 = r (V - X3) - 2 S1 J
 }
 
+// ---------------------------------------------------------------- G1 (Fp) quad gangs
+__device__ __forceinline__ void fp_sel4(fp &r, int q, const fp &a, const fp &b, const fp &c,
+                                        const fp &d) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint32_t x = q == 0 ? a.l[i] : b.l[i];
+    uint32_t y = q == 2 ? c.l[i] : d.l[i];
+    r.l[i] = q < 2 ? x : y;
+  }
+}
+// dbl-2009-l over Fp across a quad: levels X^2 Y^2 (Y+Z)^2 Z^2 | B^2 (X+B)^2 E^2 | E (D-X3)
+// (3 Fp products deep instead of 7).  r may alias p.
+__device__ __forceinline__ void gang1_dbl(g1j &r, const g1j &p, int q) {
+  fp in, s, A, B, W, Z2, E, t;
+  fp_add(t, p.y, p.z);
+  fp_sel4(in, q, p.x, p.y, t, p.z);
+  fp_sqr(s, in);
+  fp_quad_bcast<0>(A, s);
+  fp_quad_bcast<1>(B, s);
+  fp_quad_bcast<2>(W, s);
+  fp_quad_bcast<3>(Z2, s);
+  fp_add(t, p.x, B);
+  fp_sub(W, W, B);
+  fp_sub(r.z, W, Z2);  // Z3 = 2YZ
+  fp_add(E, A, A);
+  fp_add(E, E, A);     // E = 3A
+  fp_sel4(in, q, B, t, E, E);
+  fp_sqr(s, in);
+  fp C, U, F;
+  fp_quad_bcast<0>(C, s);
+  fp_quad_bcast<1>(U, s);
+  fp_quad_bcast<2>(F, s);
+  fp_sub(U, U, A);
+  fp_sub(U, U, C);
+  fp_add(U, U, U);     // D
+  fp_sub(F, F, U);
+  fp_sub(r.x, F, U);   // X3 = F - 2D
+  fp_sub(t, U, r.x);
+  fp_mul(t, E, t);     // E (D - X3), the same in every lane
+  fp_add(C, C, C);
+  fp_add(C, C, C);
+  fp_add(C, C, C);
+  fp_sub(r.y, t, C);   // Y3 = E (D - X3) - 8C
+}
+// add-2007-bl over Fp across a quad (5 Fp products deep instead of 16), r = a + b,
+// r may alias a.  The degenerate branches depend only on values the quad shares.
+__device__ __forceinline__ void gang1_add(g1j &r, const g1j &a, const g1j &b, int q) {
+  if (jac_is_inf(b)) {
+    r = a;
+    return;
+  }
+  if (jac_is_inf(a)) {
+    r = b;
+    return;
+  }
+  fp x, y, s, Z1Z1, Z2Z2, U1, U2, S1, S2;
+  fp_sel4(x, q, a.z, b.z, a.y, b.y);
+  fp_sel4(y, q, a.z, b.z, b.z, a.z);
+  fp_mul(s, x, y);
+  fp_quad_bcast<0>(Z1Z1, s);
+  fp_quad_bcast<1>(Z2Z2, s);
+  fp_quad_bcast<2>(S1, s);
+  fp_quad_bcast<3>(S2, s);
+  fp_sel4(x, q, a.x, b.x, S1, S2);
+  fp_sel4(y, q, Z2Z2, Z1Z1, Z2Z2, Z1Z1);
+  fp_mul(s, x, y);
+  fp_quad_bcast<0>(U1, s);
+  fp_quad_bcast<1>(U2, s);
+  fp_quad_bcast<2>(S1, s);
+  fp_quad_bcast<3>(S2, s);
+  fp H, R, t;
+  fp_sub(H, U2, U1);
+  fp_sub(R, S2, S1);
+  fp_add(R, R, R);
+  if (fp_is_zero(H)) {
+    if (fp_is_zero(R)) {
+      gang1_dbl(r, b, q);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  fp H2, ZZ, I, R2, Zs;
+  fp_add(H2, H, H);
+  fp_add(ZZ, a.z, b.z);
+  fp_sel4(x, q, H2, R, ZZ, ZZ);
+  fp_sqr(s, x);
+  fp_quad_bcast<0>(I, s);
+  fp_quad_bcast<1>(R2, s);
+  fp_quad_bcast<2>(Zs, s);
+  fp_sub(Zs, Zs, Z1Z1);
+  fp_sub(Zs, Zs, Z2Z2);  // 2 Z1 Z2
+  fp J, V;
+  fp_sel4(x, q, H, U1, Zs, Zs);
+  fp_sel4(y, q, I, I, H, H);
+  fp_mul(s, x, y);
+  fp_quad_bcast<0>(J, s);
+  fp_quad_bcast<1>(V, s);
+  fp_quad_bcast<2>(r.z, s);  // Z3 = 2 Z1 Z2 H
+  fp_sub(t, R2, J);
+  fp_sub(t, t, V);
+  fp_sub(r.x, t, V);         // X3 = R^2 - J - 2V
+  fp_sub(t, V, r.x);
+  fp_sel4(x, q, R, S1, R, S1);
+  fp_sel4(y, q, t, J, t, J);
+  fp_mul(s, x, y);
+  fp_quad_bcast<0>(t, s);
+  fp_quad_bcast<1>(S1, s);
+  fp_add(S1, S1, S1);
+  fp_sub(r.y, t, S1);        // Y3 = R (V - X3) - 2 S1 J
+}
+
 // [|x|]P with quad-cooperative doublings and additions
 __device__ __forceinline__ void gang_mul_by_xabs(g2j &r, const g2j &p, int q) {
   g2j acc = p;

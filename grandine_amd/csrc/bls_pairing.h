@@ -122,6 +122,46 @@ HD void line_add_aff(g2h &T, const g2a &Q, fp2 &L0, fp2 &L2, fp2 &L3) {
   fp2_mul(T.z, vvv, T.z);
 }
 
+// A G1 point prepared for line evaluation up to an Fp factor c: for Jacobian (X, Y, Z),
+// (x, y, c) = (X Z, Y, Z^3), i.e. x = xP c and y = yP c with c = Z^3; an affine point is
+// (x, y, 1) and infinity has c = 0.  The line times c is L0 c + L2 x w^2 + L3 y w^3: the
+// Fp factor c is killed by the final exponentiation, so no inversion is needed.
+struct g1s {
+  fp x, y, c;
+};
+HD void g1s_from_jac(g1s &r, const g1j &p) {
+  if (jac_is_inf(p)) {
+    fp_zero(r.x);
+    fp_zero(r.y);
+    fp_zero(r.c);
+    return;
+  }
+  fp z2;
+  fp_sqr(z2, p.z);
+  fp_mul(r.c, z2, p.z);
+  fp_mul(r.x, p.x, p.z);
+  r.y = p.y;
+}
+HD void g1s_from_aff(g1s &r, const g1a &a) {
+  r.x = a.x;
+  r.y = a.y;
+  if (aff_is_inf(a))
+    fp_zero(r.c);
+  else
+    fp_one(r.c);
+}
+HD void line_eval_s(sp034 &s, const fp2 &L0, const fp2 &L2, const fp2 &L3, const g1s &P) {
+  if (fp_is_zero(P.c)) {
+    fp2_one(s.a0);
+    fp2_zero(s.a2);
+    fp2_zero(s.a3);
+    return;
+  }
+  fp2_mul_fp(s.a0, L0, P.c);
+  fp2_mul_fp(s.a2, L2, P.x);
+  fp2_mul_fp(s.a3, L3, P.y);
+}
+
 // line at an affine G1 point (infinity gives the identity element)
 HD void line_eval(sp034 &s, const fp2 &L0, const fp2 &L2, const fp2 &L3, const g1a &P) {
   if (aff_is_inf(P)) {

@@ -240,7 +240,7 @@ struct Engine {
   std::shared_mutex reg_mu;
   size_t reg_n = 0;
   std::atomic<bool> coalesce{true};
-  size_t msm_min = 16384;  // single-segment batches at least this large use the bucket MSM
+  size_t msm_min = kMsmMinPerSeg;  // segments at least this large use the bucket MSM
 } g;
 
 // RAII lease of a context of one device: the idle context last used on the caller's
@@ -406,10 +406,12 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   const size_t np = n + nseg;
   bool single = !rands && n == nseg;  // one set per segment, r = 1
   for (size_t s = 0; single && s <= nseg; s++) single = seg_off[s] == s;
-  const bool msm = rands && nseg == 1 && n >= g.msm_min;  // bucket MSM for S
+  // bucket MSM for S when every segment is large (segment sizes >= msm_min)
+  bool msm = rands && n > 0;
+  for (size_t s = 0; msm && s < nseg; s++) msm = seg_off[s + 1] - seg_off[s] >= g.msm_min;
   MsmPlan mp{};
   if (msm) {
-    mp = msm_plan((uint32_t)n);
+    mp = msm_plan((uint32_t)n, (uint32_t)nseg);
     if (!c.ensure(c.msm, mp.bytes)) return false;
   }
   // ---- host tables, one staged upload:
@@ -430,7 +432,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   }
   const size_t ncouple = tab.size() / 2;
   const size_t chunk_off = tab.size();
-  const uint32_t CH = 4 * WGR;  // sets per level-1 G2-sum workgroup
+  const uint32_t CH = WGR;  // sets per level-1 G2-sum workgroup
   std::vector<uint32_t> seg_chunk(nseg + 1, 0);
   for (size_t s = 0; s < nseg; s++) {
     seg_chunk[s] = (uint32_t)((tab.size() - chunk_off) / 4);
@@ -482,7 +484,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     (l & 1 ? v0_n : v1_n) = std::max(l & 1 ? v0_n : v1_n, levels[l].nout);
   if (sig_groupcheck && !c.ensure(c.pre2, n * sizeof(int32_t) + 16)) return false;
   if (!c.ensure(c.U, 2 * n * sizeof(fp2) + 16) || !c.ensure(c.Q, 2 * n * sizeof(g2j) + 16) ||
-      !c.ensure(c.H, np * sizeof(g2a)) || !c.ensure(c.P, np * sizeof(g1a)) ||
+      !c.ensure(c.H, np * sizeof(g2a)) || !c.ensure(c.P, np * sizeof(g1s)) ||
       !c.ensure(c.R, 2 * n * sizeof(g2j) + 16) ||
       !c.ensure(c.gpart, nchunks * (sizeof(g2j) + 4)) || !c.ensure(c.lines, line_words * 4) ||
       !c.ensure(c.V0, ML_EVENTS * v0_n * sizeof(fp12)) ||
@@ -503,7 +505,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   HIPCHK(hipEventRecord(c.ev_pks, c.side1));
   {
     StageTimer t(S_G1MUL, c.side1);
-    launch_mv_g1mul(c.side1, pks, rands, N, c.P.as<g1a>());
+    launch_mv_g1mul(c.side1, pks, rands, N, c.P.as<g1s>());
   }
   const int32_t *pre2 = nullptr;
   if (sig_groupcheck) {
@@ -512,7 +514,8 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   }
   if (msm) {
     StageTimer t(S_G2MUL, c.side2);
-    launch_msm(c.side2, mp, c.msm.as<uint8_t>(), sigs, rands, N, c.H.as<g2a>(), c.P.as<g1a>());
+    launch_msm(c.side2, mp, c.msm.as<uint8_t>(), sigs, rands, N, T + segoff_at, empty_is_error,
+               c.H.as<g2a>(), c.P.as<g1s>(), seg_err);
   } else if (!single) {
     StageTimer t(S_G2MUL, c.side2);
     launch_mv_g2mul(c.side2, sigs, rands, N, c.R.as<g2j>());
@@ -521,13 +524,13 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   {
     StageTimer t(S_G2SUM, c.side2);
     if (msm)
-      launch_msm_flags(c.side2, pks, rands, pre, pre2, N, seg_err);
+      launch_msm_flags(c.side2, pks, rands, pre, pre2, N, T + segoff_at, NS, seg_err);
     else if (single)
-      launch_single_S(c.side2, sigs, pks, pre, pre2, N, c.P.as<g1a>(), c.H.as<g2a>(), seg_err);
+      launch_single_S(c.side2, sigs, pks, pre, pre2, N, c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
     else
       launch_g2sum(c.side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
                    T + segoff_at, NS, N, pks, rands, pre, pre2, empty_is_error, gpart, gpart_err,
-                   c.P.as<g1a>(), c.H.as<g2a>(), seg_err);
+                   c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
   }
   {
     StageTimer t(S_LINES_S, c.side2);
@@ -555,7 +558,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
   {
     StageTimer t(S_ML_LEAF, st);
-    launch_ml_leaf(st, c.lines.as<uint32_t>(), NP, c.P.as<g1a>(), T, (uint32_t)ncouple,
+    launch_ml_leaf(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T, (uint32_t)ncouple,
                    c.V0.as<fp12>());
   }
   fp12 *cur = c.V0.as<fp12>(), *other = c.V1.as<fp12>();

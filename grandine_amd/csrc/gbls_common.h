@@ -13,6 +13,9 @@ namespace gbls {
 constexpr int WG = 64;    // per-lane kernels: one wave per workgroup
 constexpr int WGR = 256;  // segment reductions: 4 waves, LDS tree
 constexpr uint32_t NONE = 0xffffffffu;
+// Launches of at least this many sets fill every SIMD with lane-per-set work, so stages
+// with a quad-gang (latency) and a lane-per-set (throughput) variant pick the latter.
+constexpr uint32_t kLaneRegimeSets = 32768;
 
 inline unsigned nblk(size_t n, unsigned per = WG) { return (unsigned)((n + per - 1) / per); }
 
@@ -43,7 +46,8 @@ void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q);
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H);
 
 // k_scalar.hip -- random-scalar products and the per-segment signature sum
-void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1a *P);
+// P_i = r_i pk_i as line-evaluation points (bls_pairing.h g1s), quad per set
+void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1s *P);
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R);
 // chunks: 4 words per level-1 workgroup {segment, half, begin, end}; seg_chunk[nseg+1].
 // seg_err[s] = a set of s failed (infinite pk, zero scalar, pre[i] != 0) or, when
@@ -51,25 +55,32 @@ void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uin
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                   const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
-                  int empty_is_error, g2j *part, int32_t *part_err, g1a *P, g2a *H,
+                  int empty_is_error, g2j *part, int32_t *part_err, g1s *P, g2a *H,
                   int32_t *seg_err);
 // single checks (r = 1, one set per segment): the extra pair of segment s is (-g1, sig_s)
 void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
-                     const int32_t *pre2, uint32_t n, g1a *P, g2a *H, int32_t *seg_err);
+                     const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err);
 
-// k_msm.hip -- S = sum r_i sig_i of one large segment by a signed-digit bucket MSM
+// k_msm.hip -- S_s = sum r_i sig_i of every segment by a signed-digit bucket MSM
 struct MsmPlan {
+  uint32_t nseg;
   int c, W;             // window bits, windows
-  uint32_t nb;          // buckets (W * 2^(c-1))
+  uint32_t nb;          // buckets (nseg * W * 2^(c-1))
   uint32_t max_chunks;  // bound on the chunk count (grid of the chunk kernel)
+  int folds;            // pairwise passes over a bucket's chunk sums
+  bool quad;            // quad-gang point operations (small launches)
   size_t o_cnt, o_start, o_cur, o_cstart, o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
 };
-MsmPlan msm_plan(uint32_t n);
-// writes the segment's extra pair (P[n] = -g1, H[n] = affine S)
+constexpr uint32_t kMsmMinPerSeg = 2048;  // default: segments at least this large use the MSM
+MsmPlan msm_plan(uint32_t n, uint32_t nseg);
+// writes each segment's extra pair (P[n + s] = -g1, H[n + s] = affine S_s), zeroes seg_err
+// and flags empty segments when empty_is_error
 void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
-                const uint64_t *rands, uint32_t n, g2a *H, g1a *P);
+                const uint64_t *rands, uint32_t n, const uint32_t *seg_off, int empty_is_error,
+                g2a *H, g1s *P, int32_t *seg_err);
 void launch_msm_flags(hipStream_t st, const g1a *pks, const uint64_t *rands, const int32_t *pre,
-                      const int32_t *pre2, uint32_t n, int32_t *seg_err);
+                      const int32_t *pre2, uint32_t n, const uint32_t *seg_off, uint32_t nseg,
+                      int32_t *seg_err);
 
 // k_lines.hip -- Miller-loop line functions of every pair
 // lines of pairs [first, first + count) of np (H indexed by pair)
@@ -77,7 +88,7 @@ void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, 
                   uint32_t *lines);
 
 // k_miller.hip -- Miller product tree + Horner
-void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1a *P,
+void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
                     const uint32_t *couples, uint32_t ncouple, fp12 *V0);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);

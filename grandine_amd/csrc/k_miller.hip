@@ -10,7 +10,7 @@
 namespace gbls {
 
 // grid (ceil(ncouple / 64), 68)
-__global__ void __launch_bounds__(WG) k_ml_leaf(const uint32_t *L, uint32_t np, const g1a *P,
+__global__ void __launch_bounds__(WG) k_ml_leaf(const uint32_t *L, uint32_t np, const g1s *P,
                                                 const uint32_t *couples, uint32_t ncouple,
                                                 fp12 *V0) {
   uint32_t c = blockIdx.x * WG + threadIdx.x;
@@ -20,13 +20,13 @@ __global__ void __launch_bounds__(WG) k_ml_leaf(const uint32_t *L, uint32_t np, 
   fp2 L0, L2, L3;
   sp034 sa, sb;
   line_get(L, np, pa, e, L0, L2, L3);
-  g1a Pa = P[pa];
-  line_eval(sa, L0, L2, L3, Pa);
+  g1s Pa = P[pa];
+  line_eval_s(sa, L0, L2, L3, Pa);
   fp12 r;
   if (pb != NONE) {
     line_get(L, np, pb, e, L0, L2, L3);
-    g1a Pb = P[pb];
-    line_eval(sb, L0, L2, L3, Pb);
+    g1s Pb = P[pb];
+    line_eval_s(sb, L0, L2, L3, Pb);
     sp_mul_sp(r, sa, sb);
   } else {
     sp_to_fp12(r, sa);
@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
   w12_store(partial + s, acc);
 }
 
-void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1a *P,
+void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
                     const uint32_t *couples, uint32_t ncouple, fp12 *V0) {
   dim3 grid(nblk(ncouple), ML_EVENTS);
   if (ncouple) k_ml_leaf<<<grid, WG, 0, st>>>(lines, np, P, couples, ncouple, V0);

@@ -9,21 +9,38 @@
 
 namespace gbls {
 
-// P_i = affine(r_i pk_i)
+// P_i = r_i pk_i as a line-evaluation point (x, y, c) = (X Z, Y, Z^3) of the Jacobian
+// result (bls_pairing.h g1s): no inversion.  One DPP quad per set, MSB-first
+// double-and-add with quad doublings / additions (bls_gang.h); lane 0 stores.
 __global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t *rands, uint32_t n,
-                                                 g1a *P) {
-  uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
+                                                 g1s *P) {
+  uint32_t u = blockIdx.x * WG + threadIdx.x;
+  uint32_t i = u >> 2;
+  int q = (int)(u & 3);
+  if (i >= n) return;  // whole quads only
   g1a pk = pks[i];
+  g1s o;
   if (!rands) {  // r = 1 (single checks): the key itself
-    P[i] = pk;
+    g1s_from_aff(o, pk);
+    if (q == 0) P[i] = o;
     return;
   }
-  g1j t;
-  mul_u64(t, pk, rands[i]);
-  g1a o;
-  jac_to_aff(o, t);
-  P[i] = o;
+  uint64_t k = rands[i];
+  g1j acc;
+  jac_set_inf(acc);
+  if (k != 0 && !aff_is_inf(pk)) {
+    int top = 63;
+    while (!((k >> top) & 1)) top--;
+    g1j base;
+    jac_from_aff(base, pk);
+    acc = base;
+    for (int b = top - 1; b >= 0; b--) {
+      gang1_dbl(acc, acc, q);
+      if ((k >> b) & 1) gang1_add(acc, acc, base, q);
+    }
+  }
+  g1s_from_jac(o, acc);
+  if (q == 0) P[i] = o;
 }
 
 // R[h * n + i] = [32-bit half h of r_i] sig_i (Jacobian); infinite signatures give the
@@ -56,47 +73,47 @@ __global__ void __launch_bounds__(WG) k_mv_g2mul(const g2a *sigs, const uint64_t
   if (q == 0) R[t] = acc;
 }
 
-template <class F>
-__device__ void wg_reduce_jac(jac<F> &v) {
-  __shared__ jac<F> buf[WGR / 2];
-  for (int w = WGR / 2; w > 0; w >>= 1) {
-    __syncthreads();
-    if (threadIdx.x >= (unsigned)w && threadIdx.x < (unsigned)2 * w) buf[threadIdx.x - w] = v;
-    __syncthreads();
-    if (threadIdx.x < (unsigned)w) {
-      jac<F> o = buf[threadIdx.x];
-      jac_add(v, v, o);
-    }
-  }
-}
 
-// level 1: workgroup c sums R[h*n + b .. h*n + e) (chunk table: {s, h, b, e}) and ORs the
-// bad flags: pk infinite (blst PAIRING_Aggregate_PK_in_G1), a zero scalar (the reference
-// only draws NonZeroU64, signature.rs:106-115; a zero would drop the set from the
-// combination, so it fails closed), or a failed pre-check
+// level 1: workgroup c sums R[h*n + b .. h*n + e) (chunk table: {s, h, b, e}, at most
+// WGR sets) with quad additions (bls_gang.h): each of the 64 quads folds a strided
+// subset, then a 6-level LDS tree joins the quads.  It also ORs the bad flags: pk
+// infinite (blst PAIRING_Aggregate_PK_in_G1), a zero scalar (the reference only draws
+// NonZeroU64, signature.rs:106-115; a zero would drop the set from the combination, so
+// it fails closed), or a failed pre-check
 __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32_t *chunks, uint32_t n,
                                                       const g1a *pks, const uint64_t *rands,
                                                       const int32_t *pre, const int32_t *pre2,
                                                       g2j *part, int32_t *part_err) {
+  constexpr int NQ = WGR / 4;
+  __shared__ g2j sh[NQ / 2];
   __shared__ int32_t e_sh;
   uint32_t c = blockIdx.x;
   uint32_t h = chunks[4 * c + 1], b = chunks[4 * c + 2], e = chunks[4 * c + 3];
+  int w = (int)(threadIdx.x >> 2), q = (int)(threadIdx.x & 3);
   if (threadIdx.x == 0) e_sh = 0;
   __syncthreads();
   g2j acc;
   jac_set_inf(acc);
   int32_t bad = 0;
-  for (uint32_t i = b + threadIdx.x; i < e; i += WGR) {
+  for (uint32_t i = b + w; i < e; i += NQ) {
     g2j r = R[(size_t)h * n + i];
-    jac_add(acc, acc, r);
-    if (h == 0)
+    gang_add(acc, acc, r, q);
+    if (h == 0 && q == 0)
       bad |= (aff_is_inf(pks[i]) || (rands && rands[i] == 0) || (pre && pre[i] != 0) ||
               (pre2 && pre2[i] != 0))
                  ? 1
                  : 0;
   }
   if (bad) atomicOr(&e_sh, 1);
-  wg_reduce_jac(acc);
+  for (int width = NQ / 2; width > 0; width >>= 1) {
+    __syncthreads();
+    if (q == 0 && w >= width && w < 2 * width) sh[w - width] = acc;
+    __syncthreads();
+    if (w < width) {
+      g2j o = sh[w];
+      gang_add(acc, acc, o, q);
+    }
+  }
   if (threadIdx.x == 0) {
     part[c] = acc;
     part_err[c] = e_sh;
@@ -111,7 +128,7 @@ __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32
 __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32_t *part_err,
                                                     const uint32_t *chunks, const uint32_t *seg_chunk,
                                                     const uint32_t *seg_off, uint32_t nseg, uint32_t n,
-                                                    int empty_is_error, g1a *P, g2a *H,
+                                                    int empty_is_error, g1s *P, g2a *H,
                                                     int32_t *seg_err) {
   constexpr int NQ = WG / 4;
   __shared__ g2j sh_lo[NQ], sh_hi[NQ];
@@ -150,9 +167,10 @@ __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32
   if (empty_is_error && seg_off[s + 1] == seg_off[s]) err = 1;
   for (int j = 0; j < 32; j++) gang_dbl(hi, hi, q);
   gang_add(lo, lo, hi, q);
-  g1a ng1;
+  g1s ng1;
   fp_set(ng1.x, k::G1X_M);
   fp_set(ng1.y, k::G1NEGY_M);
+  fp_one(ng1.c);
   g2a a;
   jac_to_aff(a, lo);
   if (q != 0) return;
@@ -164,25 +182,48 @@ __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32
 // Single checks (r_i = 1, one set per segment: verify / fast_aggregate_verify batches):
 // S_s = sig_s, so the segment's extra pair is (-g1, sig_s) -- no G2 sum, no inversion.
 __global__ void __launch_bounds__(WG) k_single_S(const g2a *sigs, const g1a *pks, const int32_t *pre,
-                                                 const int32_t *pre2, uint32_t n, g1a *P, g2a *H,
+                                                 const int32_t *pre2, uint32_t n, g1s *P, g2a *H,
                                                  int32_t *seg_err) {
   uint32_t s = blockIdx.x * WG + threadIdx.x;
   if (s >= n) return;
-  g1a ng1;
+  g1s ng1;
   fp_set(ng1.x, k::G1X_M);
   fp_set(ng1.y, k::G1NEGY_M);
+  fp_one(ng1.c);
   P[n + s] = ng1;
   H[n + s] = sigs[s];
   seg_err[s] = (aff_is_inf(pks[s]) || (pre && pre[s] != 0) || (pre2 && pre2[s] != 0)) ? 1 : 0;
 }
 
 void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
-                     const int32_t *pre2, uint32_t n, g1a *P, g2a *H, int32_t *seg_err) {
+                     const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err) {
   if (n) k_single_S<<<nblk(n), WG, 0, st>>>(sigs, pks, pre, pre2, n, P, H, seg_err);
 }
 
-void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1a *P) {
-  if (n) k_mv_g1mul<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
+// Throughput variant for large batches (every SIMD already busy): one lane per set,
+// serial formulas -- about half the instructions of the quad version.
+__global__ void __launch_bounds__(WG) k_mv_g1mul_lane(const g1a *pks, const uint64_t *rands,
+                                                      uint32_t n, g1s *P) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g1a pk = pks[i];
+  g1s o;
+  if (!rands) {
+    g1s_from_aff(o, pk);
+  } else {
+    g1j t;
+    mul_u64(t, pk, rands[i]);
+    g1s_from_jac(o, t);
+  }
+  P[i] = o;
+}
+
+void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1s *P) {
+  if (!n) return;
+  if (n >= kLaneRegimeSets)
+    k_mv_g1mul_lane<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
+  else
+    k_mv_g1mul<<<nblk(4 * (size_t)n), WG, 0, st>>>(pks, rands, n, P);
 }
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R) {
   if (n) k_mv_g2mul<<<nblk(8 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
@@ -190,7 +231,7 @@ void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uin
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                   const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
-                  int empty_is_error, g2j *part, int32_t *part_err, g1a *P, g2a *H,
+                  int empty_is_error, g2j *part, int32_t *part_err, g1s *P, g2a *H,
                   int32_t *seg_err) {
   if (nchunks)
     k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, rands, pre, pre2, part, part_err);

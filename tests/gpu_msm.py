@@ -59,6 +59,15 @@ def main():
         gpu = L.gbls_multi_verify(m, s, pks, u64(r), n) == G.SUCCESS
         ref = bool(C.ref_multi_verify(m, s, pks, u64(r), n, 16))
         res["c2"].append([name, gpu, ref])
+    # several segments at once (per-segment buckets): the 2nd and 4th corrupted
+    m2, s2, p2, r2 = F.c2_batch(3000, seed=32)
+    off = [0, 500, 1300, 1301, 2100, 3000]
+    mb = bytearray(m2)
+    mb[32 * 700] ^= 1
+    mb[32 * 1500] ^= 1
+    vs = G.i32_array(5)
+    G.check(L.gbls_multi_verify_segments(bytes(mb), s2, p2, u64(r2), 3000, G.u32_array(off), 5, vs), "segs")
+    res["segments"] = [vs[i] for i in range(5)]
     zero = list(rands)
     zero[5] = 0
     v = G.i32_array(1)

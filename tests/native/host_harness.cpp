@@ -235,7 +235,7 @@ static void pipeline(const uint8_t *msgs, const uint32_t *msg_off, const uint8_t
     uint32_t b = seg_off[s], e_ = seg_off[s + 1];
     uint32_t np = e_ - b + 1;
     std::vector<uint32_t> L((size_t)np * ML_EVENTS * 72);
-    std::vector<g1a> P(np);
+    std::vector<g1s> P(np);
     g2j S;
     jac_set_inf(S);
     int err = e_ == b;
@@ -256,9 +256,9 @@ static void pipeline(const uint8_t *msgs, const uint32_t *msg_off, const uint8_t
       std::memcpy(&pk, pks96 + 96 * i, 96);
       std::memcpy(&sig, sigs192 + 192 * i, 192);
       uint64_t r = rands ? rands[i] : 1;
-      g1j t;                                          // k_mv_g1mul
+      g1j t;                                          // k_mv_g1mul (no inversion)
       mul_u64(t, pk, r);
-      jac_to_aff(P[i - b], t);
+      g1s_from_jac(P[i - b], t);
       err |= aff_is_inf(pk) || (pre && pre[i]);
       g2j R;                                          // k_mv_g2mul
       mul_u64(R, sig, r);
@@ -267,6 +267,7 @@ static void pipeline(const uint8_t *msgs, const uint32_t *msg_off, const uint8_t
     }
     fp_set(P[np - 1].x, k::G1X_M);
     fp_set(P[np - 1].y, k::G1NEGY_M);
+    fp_one(P[np - 1].c);
     g2a Sa;
     jac_to_aff(Sa, S);
     lines_of(L.data(), np, np - 1, Sa);
@@ -279,7 +280,7 @@ static void pipeline(const uint8_t *msgs, const uint32_t *msg_off, const uint8_t
         fp2 L0, L2, L3;
         sp034 sp;
         line_get(L.data(), np, j, e, L0, L2, L3);
-        line_eval(sp, L0, L2, L3, P[j]);
+        line_eval_s(sp, L0, L2, L3, P[j]);
         fp12_mul_034(M, M, sp);
       }
       if (e == 0) {

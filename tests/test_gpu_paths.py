@@ -279,6 +279,7 @@ def test_bucket_msm_parity_subprocess():
     for name, gpu, ref in res["c2"]:
         assert gpu == ref, (name, gpu, ref)
     assert [x[1] for x in res["c2"]] == [True, False, False, True, True]
+    assert res["segments"] == [0, 5, 0, 5, 0]
     assert res["zero_scalar"] == 5
 
 
