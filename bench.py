@@ -45,25 +45,33 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # Algorithmic work per unit, in Fp products (12-limb Montgomery, 288 v_mad_u64_u32
-# each), counted from the formulas each kernel executes (BASELINE.md section 4,
-# tools/count_work.cpp).  Frozen: a faster algorithm raises the achieved fraction,
-# never lowers W.
+# each), FROZEN in BASELINE.md section 4 from tools/count_work.cpp (the engine's own
+# serial formulas compiled for the host with -DGBLS_COUNT_FPMUL; a binary-GCD inversion
+# counts as one product).  Per set unless noted.  The G2 side is priced at the reference
+# algorithm (one 64-bit r_i sig_i per set, as blst does it), so the bucket MSM doing a
+# tenth of that work raises the achieved fraction; a faster algorithm never lowers W.
 MAD_PER_FPMUL = 288
 W_FPMUL = {
-    "k_h2c_field": 0,        # SHA-256 only
-    "k_h2c_map": 2 * 1009,   # per set: 2 SSWU maps (2 sliding-window exps each) + isogeny
-    "k_h2c_clear": 2360,     # per set: Q0+Q1, 2 x [|x|] (63 dbl + 5 add), 5 adds, psi
-    "k_mv_g1mul": 1240,      # per set: 64-bit G1 double-and-add + affine
-    "k_mv_g2mul": 3150,      # per set: 64-bit G2 double-and-add
-    "k_g2sum": 48,           # per set: one Jacobian G2 add
-    "k_lines": 1530,         # per pair: 63 doubling + 5 addition line steps
-    "k_lines_S": 1530,       # per segment: the (-g1, S) pair's lines
-    "k_ml_leaf": 34 * 68 // 2,  # per pair: 68 events x (eval + half a sparse*sparse)
-    "k_ml_reduce": 54 * 68 // 2,  # per pair: 68 events x ~1/2 dense product
-    "k_ml_horner": 0,
-    "k_final_verdict": 0,
-    "k_g1_aggregate_idx": 11,  # per aggregated key: one mixed G1 addition
+    "k_h2c_field": 0,           # SHA-256 only
+    "k_h2c_map": 2110,          # 2 SSWU maps (2 Fp exponentiations each) + 3-isogeny
+    "k_h2c_clear": 2754,        # Q0+Q1, 2 x [|x|] (63 dbl + 5 add), psi, adds, affine
+    "k_mv_g1mul": 783,          # r_i pk_i: 64-bit G1 double-and-add + affine
+    "k_mv_g2mul": 1940,         # r_i sig_i: 64-bit G2 double-and-add (1897) + the sum (43)
+    "k_msm": 1940,              # the same r_i sig_i work, done as a bucket MSM
+    "k_g2sum": 43,              # one Jacobian G2 addition
+    "k_lines": 1508,            # per pair: 63 doubling + 5 addition line steps
+    "k_lines_S": 1508,          # per segment: the (-g1, S) pair's lines
+    "k_ml_group": 2924,         # per pair: 68 events x (line evaluation 4 + sparse-dense product 39)
+    "k_ml_reduce": 0,           # per pair: counted in k_ml_group (the wave levels fold <= 1/G of it)
+    "k_ml_horner": 6030,        # per segment: 67 Fp12 squarings + 67 products
+    "k_final_verdict": 13357,   # per segment: final exponentiation
+    "k_g1_aggregate_idx": 11,   # per aggregated key: one mixed G1 addition
 }
+W_PAIR = W_FPMUL["k_lines"] + 884 + 1836  # lines + round-1 leaf + tree (frozen)      # 4228
+W_SEGMENT = W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"] + W_PAIR          # 23615
+W_SET = (W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"] + W_FPMUL["k_mv_g1mul"]
+         + W_FPMUL["k_mv_g2mul"] + W_PAIR)                                            # 11815
+W_G2_CHECK = 1251  # sigma subgroup check (fast_aggregate_verify)
 
 
 def cpu_threads():
@@ -270,8 +278,12 @@ def main():
         def verdict_ok():
             return all(bool((v == G.SUCCESS).all()) for v in (d_verdicts if world == 1 else [d_verdict]))
 
-        leg.stage_units = lambda s: {"k_ml_leaf": n + nb, "k_ml_reduce": n + nb, "k_lines_S": nb,
+        leg.stage_units = lambda s: {"k_ml_group": n + nb, "k_ml_reduce": n + nb, "k_lines_S": nb,
+                                     "k_ml_horner": nb, "k_final_verdict": nb,
                                      "k_g1_aggregate_idx": getattr(leg, "pks_per_step", n)}.get(s, n)
+        # whole step, frozen W: sets + per-batch pair/Horner/final exp + key aggregation
+        leg.path_fpmul = lambda: (n * W_SET + nb * W_SEGMENT
+                                  + (getattr(leg, "pks_per_step", n) - n) * W_FPMUL["k_g1_aggregate_idx"])
     # ------------------------------------------------------------------ C3
     elif cfg == "C3":
         m = args.sets or 10_000
@@ -306,8 +318,13 @@ def main():
         def verdict_ok():
             return bool(torch.equal(d_v.cpu(), want))
 
-        leg.stage_units = lambda s: {"k_g1_aggregate_idx": m * k, "k_lines_S": m, "k_ml_leaf": 2 * m,
+        leg.stage_units = lambda s: {"k_g1_aggregate_idx": m * k, "k_lines_S": m, "k_ml_group": 2 * m,
                                      "k_ml_reduce": 2 * m}.get(s, m)
+        # per message: key aggregation, sigma subgroup check, hash_to_G2, 2 pairs, Horner,
+        # final exponentiation
+        leg.path_fpmul = lambda: m * ((k - 1) * W_FPMUL["k_g1_aggregate_idx"] + W_G2_CHECK
+                                      + W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"] + 2 * W_PAIR
+                                      + W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"])
     # ------------------------------------------------------------------ C1 (latency, host ABI)
     else:
         return bench_c1(args, L, G, F, np)
@@ -395,6 +412,10 @@ def main():
                 "frac": round(ach / (peak / 1e12), 5) if peak else None,
                 "traffic": pmc_traffic(dom, leg.units) if cfg == "C2" else None,
                 "avg_launch_ms": round(tot_ms / ncalls, 4),
+                "path": {"fpmul_per_step": leg.path_fpmul(),
+                         "achieved": round(leg.path_fpmul() * MAD_PER_FPMUL * args.steps / dt / 1e12, 4),
+                         "frac": round(leg.path_fpmul() * MAD_PER_FPMUL * args.steps / dt / peak, 5)
+                         if peak else None},
                 "stage_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()}}
 
     if rank == 0:

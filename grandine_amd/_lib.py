@@ -12,6 +12,8 @@ import os
 import threading
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgrandine_bls.so")
+# experiment builds (tools/): another in-tree build of the same library
+LIB_PATH = os.environ.get("GBLS_LIB", LIB_PATH)
 
 # status codes (BLST_ERROR mirror)
 SUCCESS = 0

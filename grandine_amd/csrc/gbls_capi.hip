@@ -82,12 +82,12 @@ struct Buf {
 // ---- optional per-stage timing (HIP events on the launch stream), for bench.py
 enum Stage {
   S_H2C_FIELD, S_H2C_MAP, S_H2C_CLEAR, S_G1MUL, S_G2MUL, S_G2SUM, S_LINES, S_LINES_S, S_ML_LEAF,
-  S_ML_REDUCE, S_ML_HORNER, S_FINAL, S_PK_GATHER, S_COUNT
+  S_ML_REDUCE, S_ML_HORNER, S_FINAL, S_PK_GATHER, S_MSM, S_COUNT
 };
 const char *kStageNames[S_COUNT] = {"k_h2c_field", "k_h2c_map",   "k_h2c_clear", "k_mv_g1mul",
                                     "k_mv_g2mul",  "k_g2sum",      "k_lines",     "k_lines_S",
-                                    "k_ml_leaf",   "k_ml_reduce",  "k_ml_horner", "k_final_verdict",
-                                    "k_g1_aggregate_idx"};
+                                    "k_ml_group",  "k_ml_reduce",  "k_ml_horner", "k_final_verdict",
+                                    "k_g1_aggregate_idx", "k_msm"};
 
 struct Prof {
   std::mutex mu;
@@ -397,13 +397,12 @@ bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t s
 // signature (verify / fast_aggregate_verify, signature.rs:51,86).  Streams:
 //   side 1: key resolution (gather / aggregation) -> r_i pk_i
 //   side 2: signature group check, then S = sum r_i sig_i (waits for the keys' flags),
-//           then the lines of the (-g1, S) pairs
+//           then the lines of the (-g1, S) pairs (or of the MSM's weighted bucket sums)
 //   main:   hash_to_G2 -> the sets' lines;  join -> Miller product tree -> partials
 bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *msg_off,
                        const g2a *sigs, const PkSource &src, const uint64_t *rands,
                        bool sig_groupcheck, size_t n, const uint32_t *seg_off, size_t nseg,
                        int empty_is_error, fp12 *partials, int32_t *seg_err, hipStream_t st) {
-  const size_t np = n + nseg;
   bool single = !rands && n == nseg;  // one set per segment, r = 1
   for (size_t s = 0; single && s <= nseg; s++) single = seg_off[s] == s;
   // bucket MSM for S when every segment is large (segment sizes >= msm_min)
@@ -414,23 +413,45 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     mp = msm_plan((uint32_t)n, (uint32_t)nseg);
     if (!c.ensure(c.msm, mp.bytes)) return false;
   }
+  // extra Miller pairs per segment after the n sets: (-g1, S), or the MSM's weighted
+  // bucket / window sums
+  const size_t X = msm ? mp.extra : 1;
+  const size_t np = n + nseg * X;
   // ---- host tables, one staged upload:
-  //   [couples][g2 chunks][seg_chunk][reduction levels][seg_off]
+  //   [pair list][groups][g2 chunks][seg_chunk][reduction levels][seg_off]
+  // Level 0 of the Miller product: per segment, its pairs (sets, then the extra pairs)
+  // in groups of <= G, strided so that a wave's lanes read adjacent pairs (k_ml_group).
+  // G: the largest power of two <= 64 that still gives >= 65536 lanes (one wave per
+  // SIMD) over the 68 events.
+  uint32_t G = 1;
+  while (G < 64 && (uint64_t)ML_EVENTS * np / (2 * G) >= 65536) G *= 2;
   std::vector<uint32_t> &tab = c.host_tab;
   tab.clear();
+  tab.resize(np);
   std::vector<uint32_t> cnt(nseg);
-  for (size_t s = 0; s < nseg; s++) {  // level-0 couples of each segment's pair list
-    uint32_t b = seg_off[s], e = seg_off[s + 1];
-    uint32_t len = e - b + 1;  // + the segment's (-g1, S) pair at n + s
-    for (uint32_t j = 0; j < len; j += 2) {
-      uint32_t x = j < e - b ? b + j : (uint32_t)(n + s);
-      uint32_t y = j + 1 < len ? (j + 1 < e - b ? b + j + 1 : (uint32_t)(n + s)) : NONE;
-      tab.push_back(x);
-      tab.push_back(y);
-      cnt[s]++;
+  {
+    size_t at = 0;
+    for (size_t s = 0; s < nseg; s++) {
+      for (uint32_t i = seg_off[s]; i < seg_off[s + 1]; i++) tab[at++] = i;
+      for (size_t k = 0; k < X; k++) tab[at++] = (uint32_t)(n + s * X + k);
     }
   }
-  const size_t ncouple = tab.size() / 2;
+  const size_t grp_off = tab.size();
+  {
+    uint32_t at = 0;
+    for (size_t s = 0; s < nseg; s++) {
+      uint32_t m = seg_off[s + 1] - seg_off[s] + (uint32_t)X;
+      uint32_t ng = (m + G - 1) / G;
+      for (uint32_t k = 0; k < ng; k++) {
+        tab.push_back(at + k);
+        tab.push_back(ng);
+        tab.push_back((m - k + ng - 1) / ng);
+      }
+      cnt[s] = ng;
+      at += m;
+    }
+  }
+  const size_t ngroup = (tab.size() - grp_off) / 3;
   const size_t chunk_off = tab.size();
   const uint32_t CH = WGR;  // sets per level-1 G2-sum workgroup
   std::vector<uint32_t> seg_chunk(nseg + 1, 0);
@@ -456,7 +477,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     size_t tab_off, nin, nout;
   };
   std::vector<Level> levels;
-  size_t cur_n = ncouple;
+  size_t cur_n = ngroup;
   while (*std::max_element(cnt.begin(), cnt.end()) > 1) {
     Level L{tab.size(), cur_n, 0};
     size_t in_base = 0;
@@ -479,7 +500,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   tab.insert(tab.end(), seg_off, seg_off + nseg + 1);
   // ---- workspaces
   const size_t line_words = (size_t)np * ML_EVENTS * 72;
-  size_t v1_n = 1, v0_n = ncouple;
+  size_t v1_n = 1, v0_n = ngroup;
   for (size_t l = 0; l < levels.size(); l++)
     (l & 1 ? v0_n : v1_n) = std::max(l & 1 ? v0_n : v1_n, levels[l].nout);
   if (sig_groupcheck && !c.ensure(c.pre2, n * sizeof(int32_t) + 16)) return false;
@@ -512,20 +533,19 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     launch_g2_check(c.side2, sigs, N, c.pre2.as<int32_t>(), 0);
     pre2 = c.pre2.as<int32_t>();
   }
-  if (msm) {
-    StageTimer t(S_G2MUL, c.side2);
-    launch_msm(c.side2, mp, c.msm.as<uint8_t>(), sigs, rands, N, T + segoff_at, empty_is_error,
-               c.H.as<g2a>(), c.P.as<g1s>(), seg_err);
+  if (msm) {  // the keys' flags are read by the first MSM kernel
+    HIPCHK(hipStreamWaitEvent(c.side2, c.ev_pks, 0));
+    StageTimer t(S_MSM, c.side2);
+    launch_msm(c.side2, mp, c.msm.as<uint8_t>(), sigs, rands, pks, pre, pre2, N, T + segoff_at,
+               empty_is_error, c.H.as<g2a>(), c.P.as<g1s>(), seg_err);
   } else if (!single) {
     StageTimer t(S_G2MUL, c.side2);
     launch_mv_g2mul(c.side2, sigs, rands, N, c.R.as<g2j>());
   }
-  HIPCHK(hipStreamWaitEvent(c.side2, c.ev_pks, 0));
-  {
+  if (!msm) {
+    HIPCHK(hipStreamWaitEvent(c.side2, c.ev_pks, 0));
     StageTimer t(S_G2SUM, c.side2);
-    if (msm)
-      launch_msm_flags(c.side2, pks, rands, pre, pre2, N, T + segoff_at, NS, seg_err);
-    else if (single)
+    if (single)
       launch_single_S(c.side2, sigs, pks, pre, pre2, N, c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
     else
       launch_g2sum(c.side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
@@ -534,7 +554,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   }
   {
     StageTimer t(S_LINES_S, c.side2);
-    launch_lines(c.side2, c.H.as<g2a>(), N, NS, NP, c.lines.as<uint32_t>());
+    launch_lines(c.side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, c.lines.as<uint32_t>());
   }
   {
     StageTimer t(S_H2C_FIELD, st);
@@ -558,8 +578,8 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
   {
     StageTimer t(S_ML_LEAF, st);
-    launch_ml_leaf(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T, (uint32_t)ncouple,
-                   c.V0.as<fp12>());
+    launch_ml_group(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T, T + grp_off,
+                    (uint32_t)ngroup, c.V0.as<fp12>());
   }
   fp12 *cur = c.V0.as<fp12>(), *other = c.V1.as<fp12>();
   {

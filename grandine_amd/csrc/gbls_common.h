@@ -69,18 +69,20 @@ struct MsmPlan {
   uint32_t max_chunks;  // bound on the chunk count (grid of the chunk kernel)
   int folds;            // pairwise passes over a bucket's chunk sums
   bool quad;            // quad-gang point operations (small launches)
+  bool tree;            // per-window bucket trees (c = 13) or per-bucket pairs (c = 5)
+  uint32_t extra;       // extra Miller pairs per segment: W (tree) or W * 2^(c-1)
   size_t o_cnt, o_start, o_cur, o_cstart, o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
 };
 constexpr uint32_t kMsmMinPerSeg = 2048;  // default: segments at least this large use the MSM
 MsmPlan msm_plan(uint32_t n, uint32_t nseg);
-// writes each segment's extra pair (P[n + s] = -g1, H[n + s] = affine S_s), zeroes seg_err
-// and flags empty segments when empty_is_error
+// writes each segment's p.extra Miller pairs (P[n + s * extra + k] = a constant G1 weight,
+// H[...] = affine bucket or window sum), zeroes seg_err and flags empty segments when
+// empty_is_error
+// (pks, pre, pre2: the segment error flags of k_msm_count, as k_g2sum_final sets them)
 void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
-                const uint64_t *rands, uint32_t n, const uint32_t *seg_off, int empty_is_error,
-                g2a *H, g1s *P, int32_t *seg_err);
-void launch_msm_flags(hipStream_t st, const g1a *pks, const uint64_t *rands, const int32_t *pre,
-                      const int32_t *pre2, uint32_t n, const uint32_t *seg_off, uint32_t nseg,
-                      int32_t *seg_err);
+                const uint64_t *rands, const g1a *pks, const int32_t *pre, const int32_t *pre2,
+                uint32_t n, const uint32_t *seg_off, int empty_is_error, g2a *H, g1s *P,
+                int32_t *seg_err);
 
 // k_lines.hip -- Miller-loop line functions of every pair
 // lines of pairs [first, first + count) of np (H indexed by pair)
@@ -88,8 +90,9 @@ void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, 
                   uint32_t *lines);
 
 // k_miller.hip -- Miller product tree + Horner
-void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
-                    const uint32_t *couples, uint32_t ncouple, fp12 *V0);
+// groups: (first index into plist, stride, count) per group, segment by segment
+void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
+                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, fp12 *V0);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);
 void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial);

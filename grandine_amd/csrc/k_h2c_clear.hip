@@ -3,7 +3,8 @@
 // One DPP quad (4 lanes) per message: the doublings and additions run quad-cooperatively
 // (bls_gang.h); psi and the affine conversion run
 // redundantly in all four lanes and lane 0 stores.  Output: affine points (Miller-loop
-// input).
+// input).  Launches of at least kLaneRegimeSets messages run one message per lane
+// (k_h2c_clear_lane: a quarter of the instructions per message, the chip already full).
 #include "gbls_common.h"
 #include "bls_gang.h"
 
@@ -45,8 +46,24 @@ __global__ void __launch_bounds__(WG) k_h2c_clear(const g2j *Q, uint32_t n, g2a 
   if (q == 0) H[i] = o;
 }
 
+// one lane per message (serial clear_cofactor_g2): for launches that fill the chip
+__global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n, g2a *H) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g2j a = Q[2 * i], b = Q[2 * i + 1], h;
+  jac_add(a, a, b);
+  clear_cofactor_g2(h, a);
+  g2a o;
+  jac_to_aff(o, h);
+  H[i] = o;
+}
+
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
-  if (n) k_h2c_clear<<<nblk((size_t)n * 4), WG, 0, st>>>(Q, n, H);
+  if (!n) return;
+  if (n >= kLaneRegimeSets)
+    k_h2c_clear_lane<<<nblk(n), WG, 0, st>>>(Q, n, H);
+  else
+    k_h2c_clear<<<nblk((size_t)n * 4), WG, 0, st>>>(Q, n, H);
 }
 
 }  // namespace gbls

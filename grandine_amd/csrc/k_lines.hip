@@ -2,7 +2,8 @@
 // along |x|) of every pair's G2 point, stored structure-of-arrays (bls_pairing.h
 // line_word) so that each later load is one coalesced dword per lane.  One DPP quad per
 // pair: doubling and addition steps run quad-cooperatively (bls_gang.h gang_line_dbl,
-// gang_line_add_aff); lane q stores line components c with c % 4 == q.
+// gang_line_add_aff); lane q stores line components c with c % 4 == q.  Launches of at
+// least kLaneRegimeSets pairs run one pair per lane instead (k_lines_lane).
 #include "gbls_common.h"
 #define GBLS_GANG_LINES
 #include "bls_gang.h"
@@ -52,9 +53,23 @@ __global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t first, uint
   }
 }
 
+// one lane per pair (serial lines_of): a quarter of the quad's instructions per pair, for
+// launches that fill the chip on their own
+__global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first, uint32_t count,
+                                                   uint32_t np, uint32_t *L) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= count) return;
+  g2a Q = H[first + i];
+  lines_of(L, np, first + i, Q);
+}
+
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
                   uint32_t *lines) {
-  if (count) k_lines<<<nblk((size_t)count * 4), WG, 0, st>>>(H, first, count, np, lines);
+  if (!count) return;
+  if (count >= kLaneRegimeSets)
+    k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, np, lines);
+  else
+    k_lines<<<nblk((size_t)count * 4), WG, 0, st>>>(H, first, count, np, lines);
 }
 
 }  // namespace gbls

@@ -1,6 +1,11 @@
 // gfx950 kernels: the batch Miller product as a tree (bls_pairing.h header comment).
-//   k_ml_leaf   lane per (event e, couple of pairs): line_e(P_a) * line_e(P_b)
-//               (two sparse evaluations, 6 Fp2 products) -> dense Fp12
+//   k_ml_group  lane per (event e, group of <= G pairs of one segment): the product of
+//               the group's evaluated lines, line_e(P_a) line_e(P_b) ... (sparse x sparse,
+//               then dense x sparse), in registers -> one dense Fp12.  A group's pairs are
+//               strided through its segment's pair list (pair k, k + ng, k + 2 ng, ...
+//               for ng groups), so lanes of a wave load the SoA line words of adjacent
+//               pairs: coalesced.  G grows with the batch (bigger G = fewer values for
+//               the wave-cooperative levels, which are 3x less efficient per product).
 //   k_ml_reduce wave per (event, group of <= 4 values of one segment): wave-cooperative
 //               Fp12 products (bls_wave12.h)
 //   k_ml_horner wave per segment: Horner over the 68 events, then conj (x < 0)
@@ -9,29 +14,36 @@
 
 namespace gbls {
 
-// grid (ceil(ncouple / 64), 68)
-__global__ void __launch_bounds__(WG) k_ml_leaf(const uint32_t *L, uint32_t np, const g1s *P,
-                                                const uint32_t *couples, uint32_t ncouple,
-                                                fp12 *V0) {
-  uint32_t c = blockIdx.x * WG + threadIdx.x;
-  int e = blockIdx.y;
-  if (c >= ncouple) return;
-  uint32_t pa = couples[2 * c], pb = couples[2 * c + 1];
+__device__ __forceinline__ void ml_eval(sp034 &s, const uint32_t *L, uint32_t np, const g1s *P,
+                                        uint32_t pair, int e) {
   fp2 L0, L2, L3;
+  line_get(L, np, pair, e, L0, L2, L3);
+  g1s Pp = P[pair];
+  line_eval_s(s, L0, L2, L3, Pp);
+}
+
+// grid (ceil(ngroup / 64), 68); group g = (first plist index, stride, count)
+__global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np, const g1s *P,
+                                                 const uint32_t *plist, const uint32_t *grp,
+                                                 uint32_t ngroup, fp12 *V0) {
+  uint32_t g = blockIdx.x * WG + threadIdx.x;
+  int e = blockIdx.y;
+  if (g >= ngroup) return;
+  uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
   sp034 sa, sb;
-  line_get(L, np, pa, e, L0, L2, L3);
-  g1s Pa = P[pa];
-  line_eval_s(sa, L0, L2, L3, Pa);
-  fp12 r;
-  if (pb != NONE) {
-    line_get(L, np, pb, e, L0, L2, L3);
-    g1s Pb = P[pb];
-    line_eval_s(sb, L0, L2, L3, Pb);
-    sp_mul_sp(r, sa, sb);
+  fp12 acc;
+  ml_eval(sa, L, np, P, plist[at], e);
+  if (cnt == 1) {
+    sp_to_fp12(acc, sa);
   } else {
-    sp_to_fp12(r, sa);
+    ml_eval(sb, L, np, P, plist[at + stride], e);
+    sp_mul_sp(acc, sa, sb);
+    for (uint32_t j = 2; j < cnt; j++) {
+      ml_eval(sa, L, np, P, plist[at + j * stride], e);
+      fp12_mul_034(acc, acc, sa);
+    }
   }
-  V0[(size_t)e * ncouple + c] = r;
+  V0[(size_t)e * ngroup + g] = acc;
 }
 
 // copy one Fp12 image global <-> LDS with all 64 lanes
@@ -79,10 +91,10 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
   w12_store(partial + s, acc);
 }
 
-void launch_ml_leaf(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
-                    const uint32_t *couples, uint32_t ncouple, fp12 *V0) {
-  dim3 grid(nblk(ncouple), ML_EVENTS);
-  if (ncouple) k_ml_leaf<<<grid, WG, 0, st>>>(lines, np, P, couples, ncouple, V0);
+void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
+                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, fp12 *V0) {
+  dim3 grid(nblk(ngroup), ML_EVENTS);
+  if (ngroup) k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, V0);
 }
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout) {

@@ -3,26 +3,37 @@
 // 64-bit POINTonE2_mult_w5 per set) as a bucket (Pippenger) multi-scalar multiplication,
 // per segment of batches whose segments hold >= kMsmMinPerSeg sets (the C5-scale shards,
 // coalesced C2 batches), where it replaces the per-set double-and-add of k_mv_g2mul and
-// the chunk sums of k_g2sum: about W additions per set instead of 64 doublings + 32
-// additions.  Point operations run on DPP quads (bls_gang.h) when the launch is small
-// (latency regime) and one per lane when it fills the chip.
+// the chunk sums of k_g2sum: about W mixed additions per set instead of 64 doublings +
+// 32 additions.
 //
-// Signed c-bit digits, W = ceil(65 / c) windows, B = 2^(c-1) buckets per window and
-// segment (digit d != 0 adds sign(d) sig into bucket |d| - 1 of its segment's window):
-//   1 k_msm_count    lane per set: bucket histogram (atomics)
+// Signed c-bit digits, W = 65 / c windows, B = 2^(c-1) buckets per window and segment
+// (digit d != 0 adds sign(d) sig into bucket |d| - 1 of its segment's window):
+//   1 k_msm_count    lane per set: bucket histogram (atomics), segment error flags
 //   2 k_msm_scan     one workgroup: bucket starts, chunk starts (K entries per chunk)
 //   3 k_msm_scatter  lane per set: (set | sign) into its buckets' lists
-//   4 k_msm_chunk    per chunk: sum of <= K affine points
-//   5 k_msm_fold     per-bucket pairwise reduction of the chunk sums (log passes);
-//     k_msm_bucket   the bucket sums as level-0 tree nodes
-//   6 k_msm_tree     per (segment, window), a binary tree over the buckets computing
+//   4 k_msm_chunk    lane per chunk: sum of <= K affine points (mixed additions)
+//   5 k_msm_fold     per-bucket pairwise reduction of the chunk sums (log passes; DPP
+//                    quads when the launch is small, one lane per addition otherwise)
+// The bucket sums X_{w,b} never go through a Horner chain of 60 doublings.  The weights
+// move to the G1 side of the pairing instead, where they are constants:
+//   e(-g1, S) = prod_{w,b} e(-[(b+1) 2^(c w)] g1, X_{w,b}),
+// so every bucket becomes one extra Miller pair of its segment, with a precomputed G1
+// point (bls_constants.h MSM_W5, tools/gen_constants.py).  With c = 5 that is
+// 13 * 16 = 208 pairs per segment (+5% Miller work at 4096 sets), and the G2 side has
+// no serial tail:
+//   6 k_msm_pairs    lane per bucket: affine X_{w,b}, its pair
+// With c = 13 (segments >= 2^16 sets, 4096 buckets per window) a per-window tree
+// first folds the weights (b + 1) into S_w, and the 5 window sums pair with
+// -[2^(13 w)] g1 (MSM_W13):
+//   6 k_msm_bucket   level-0 tree nodes
+//   7 k_msm_tree     per (segment, window), a binary tree over the buckets computing
 //                    S_w = sum_b (b+1) X_b with nodes (T = sum X, A = sum (b - lo) X):
 //                    T = T_L + T_R, A = A_L + A_R + 2^l T_R   (l = level)
-//   7 k_msm_final    quad per segment: S = sum_w 2^(c w) S_w (Horner), affine, the
-//                    segment's extra pair (-g1, S)
+//   8 k_msm_wpairs   lane per window: affine S_w = A + T, its pair
 // Infinite signatures and zero scalars contribute nothing (blst skips infinite
-// signatures; a zero scalar fails the batch through k_msm_flags).  Bucket order is
-// nondeterministic (atomics) but the sum is exact, so S is bit-exact.
+// signatures; a zero scalar fails the batch through k_msm_count's flags).  An empty bucket is
+// the point at infinity, whose Miller pair is the identity.  Bucket order is
+// nondeterministic (atomics) but the sums are exact, so the verdict is too.
 #include "gbls_common.h"
 #include "bls_gang.h"
 
@@ -54,15 +65,22 @@ __device__ __forceinline__ uint32_t msm_segment(const uint32_t *seg_off, uint32_
   return lo;
 }
 
+// also the per-segment error flags: an infinite key, a zero scalar or a failed
+// pre-check (key aggregation / signature group check) fails the set's segment
 __global__ void __launch_bounds__(WGR) k_msm_count(const g2a *sigs, const uint64_t *rands, uint32_t n,
                                                    const uint32_t *seg_off, uint32_t nseg, int c,
-                                                   int W, uint32_t *cnt) {
+                                                   int W, const g1a *pks, const int32_t *pre,
+                                                   const int32_t *pre2, uint32_t *cnt,
+                                                   int32_t *seg_err) {
   uint32_t i = blockIdx.x * WGR + threadIdx.x;
   if (i >= n) return;
   uint64_t k = rands[i];
+  const uint32_t s = msm_segment(seg_off, nseg, i);
+  if (aff_is_inf(pks[i]) || k == 0 || (pre && pre[i] != 0) || (pre2 && pre2[i] != 0))
+    atomicOr(&seg_err[s], 1);
   if (k == 0 || aff_is_inf(sigs[i])) return;
   const uint32_t B = 1u << (c - 1);
-  const uint32_t base = msm_segment(seg_off, nseg, i) * (uint32_t)W * B;
+  const uint32_t base = s * (uint32_t)W * B;
   uint32_t carry = 0;
   for (int w = 0; w < W; w++) {
     int d = msm_digit(k, w, c, carry);
@@ -133,7 +151,7 @@ __global__ void __launch_bounds__(WGR) k_msm_scatter(const g2a *sigs, const uint
   }
 }
 
-// point operations of the MSM kernels: on a DPP quad (Q, latency regime) or one lane
+// point additions of the fold passes: on a DPP quad (Q, latency regime) or one lane
 template <bool Q>
 __device__ __forceinline__ void p_add(g2j &r, const g2j &a, const g2j &b, int q) {
   if (Q) {
@@ -144,13 +162,6 @@ __device__ __forceinline__ void p_add(g2j &r, const g2j &a, const g2j &b, int q)
   }
 }
 template <bool Q>
-__device__ __forceinline__ void p_dbl(g2j &r, const g2j &a, int q) {
-  if (Q)
-    gang_dbl(r, a, q);
-  else
-    jac_dbl(r, a);
-}
-template <bool Q>
 __device__ __forceinline__ uint32_t p_unit(int &q) {
   uint32_t t = blockIdx.x * WG + threadIdx.x;
   q = Q ? (int)(t & 3) : 0;
@@ -158,13 +169,11 @@ __device__ __forceinline__ uint32_t p_unit(int &q) {
 }
 
 // chunk j: sum of <= K affine points of one bucket (found by binary search over cstart)
-template <bool Q>
 __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_t *list,
                                                   const uint32_t *start, const uint32_t *cstart,
                                                   uint32_t nb, uint32_t max_chunks, g2j *chunk) {
-  int q;
-  uint32_t j = p_unit<Q>(q);
-  if (j >= max_chunks || j >= cstart[nb]) return;  // whole quads
+  uint32_t j = blockIdx.x * WG + threadIdx.x;
+  if (j >= max_chunks || j >= cstart[nb]) return;
   uint32_t lo = 0, hi = nb;  // largest b with cstart[b] <= j
   while (hi - lo > 1) {
     uint32_t mid = (lo + hi) >> 1;
@@ -182,15 +191,9 @@ __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_
     uint32_t v = list[e];
     g2a p = sigs[v & 0x7fffffffu];
     if (v >> 31) fp2_neg(p.y, p.y);
-    if (Q) {
-      g2j pj;
-      jac_from_aff(pj, p);
-      gang_add(acc, acc, pj, q);
-    } else {
-      jac_add_aff(acc, acc, p);
-    }
+    jac_add_aff(acc, acc, p);
   }
-  if (q == 0) chunk[j] = acc;
+  chunk[j] = acc;
 }
 
 // pass p of the per-bucket pairwise reduction of chunk sums: chunk k of bucket b (k a
@@ -217,6 +220,39 @@ __global__ void __launch_bounds__(WG) k_msm_fold(const uint32_t *cstart, uint32_
   if (q == 0) chunk[j] = a;
 }
 
+// the constant G1 half of an extra pair: table entry k (x, y Montgomery), c = 1
+__device__ __forceinline__ void msm_weight(g1s &o, const uint32_t *table, uint32_t k) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    o.x.l[i] = table[24 * k + i];
+    o.y.l[i] = table[24 * k + 12 + i];
+  }
+  fp_one(o.c);
+}
+
+// c = 5: lane per bucket t = s * W * B + k; its sum X (the bucket's folded first chunk, or
+// infinity) pairs with -[(b+1) 2^(c w)] g1 at pair n + t
+__global__ void __launch_bounds__(WG) k_msm_pairs(const g2j *chunk, const uint32_t *cstart,
+                                                  uint32_t nb, uint32_t per_seg, uint32_t n,
+                                                  const uint32_t *seg_off, int empty_is_error,
+                                                  g1s *P, g2a *H, int32_t *seg_err) {
+  uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= nb) return;
+  uint32_t s = t / per_seg, k = t % per_seg;
+  g2j x;
+  if (cstart[t + 1] > cstart[t])
+    x = chunk[cstart[t]];
+  else
+    jac_set_inf(x);
+  g2a a;
+  jac_to_aff(a, x);
+  g1s w;
+  msm_weight(w, k::MSM_W5, k);
+  P[n + t] = w;
+  H[n + t] = a;
+  if (k == 0 && empty_is_error && seg_off[s + 1] == seg_off[s]) atomicOr(&seg_err[s], 1);
+}
+
 // level-0 tree nodes: T = X_b (the bucket's folded first chunk, or infinity), A = inf
 __global__ void __launch_bounds__(WG) k_msm_bucket(const g2j *chunk, const uint32_t *cstart,
                                                    uint32_t nb, g2j *T, g2j *A) {
@@ -231,78 +267,57 @@ __global__ void __launch_bounds__(WG) k_msm_bucket(const g2j *chunk, const uint3
 // tree level l: nodes (T, A) of ranges of 2^l buckets -> ranges of 2^(l+1); per
 // (segment, window) group g the level has m = B >> (l+1) output nodes: inputs at
 // g * 2m + 2q (+1), output at g * m + q.
-template <bool Q>
 __global__ void __launch_bounds__(WG) k_msm_tree(const g2j *Tin, const g2j *Ain, uint32_t groups,
                                                  uint32_t m, int l, g2j *Tout, g2j *Aout) {
-  int q;
-  uint32_t t = p_unit<Q>(q);
+  uint32_t t = blockIdx.x * WG + threadIdx.x;
   if (t >= groups * m) return;
   uint32_t g = t / m, k2 = t % m;
   size_t li = (size_t)g * 2 * m + 2 * k2;
   g2j TL = Tin[li], TR = Tin[li + 1], AL = Ain[li], AR = Ain[li + 1];
-  p_add<Q>(AL, AL, AR, q);
+  jac_add(AL, AL, AR);
   g2j x = TR;
-  for (int i = 0; i < l; i++) p_dbl<Q>(x, x, q);
-  p_add<Q>(AL, AL, x, q);
-  p_add<Q>(TL, TL, TR, q);
-  if (q != 0) return;
+  for (int i = 0; i < l; i++) jac_dbl(x, x);
+  jac_add(AL, AL, x);
+  jac_add(TL, TL, TR);
   Tout[t] = TL;
   Aout[t] = AL;
 }
 
-// quad per segment: S_w = A_w + T_w (weights b + 1), S = sum_w 2^(c w) S_w, affine; the
-// segment's extra Miller pair (-g1, S) at index n + s; an empty segment is flagged when
-// empty_is_error
-__global__ void __launch_bounds__(WG) k_msm_final(const g2j *T, const g2j *A, uint32_t nseg, int W,
-                                                  int c, uint32_t n, const uint32_t *seg_off,
-                                                  int empty_is_error, g1s *P, g2a *H,
-                                                  int32_t *seg_err) {
-  uint32_t s = (blockIdx.x * WG + threadIdx.x) >> 2;
-  int q = (int)(threadIdx.x & 3);
-  if (s >= nseg) return;
-  g2j acc;
-  jac_set_inf(acc);
-  for (int w = W - 1; w >= 0; w--) {
-    for (int i = 0; i < c && w != W - 1; i++) gang_dbl(acc, acc, q);
-    g2j a = A[(size_t)s * W + w], t = T[(size_t)s * W + w];
-    gang_add(a, a, t, q);
-    gang_add(acc, acc, a, q);
-  }
-  g2a a;
-  jac_to_aff(a, acc);
-  if (q != 0) return;
-  g1s ng1;
-  fp_set(ng1.x, k::G1X_M);
-  fp_set(ng1.y, k::G1NEGY_M);
-  fp_one(ng1.c);
-  P[n + s] = ng1;
-  H[n + s] = a;
-  if (empty_is_error && seg_off[s + 1] == seg_off[s]) atomicOr(&seg_err[s], 1);
-}
-
-// per-segment error flags: an infinite key, a zero scalar or a failed pre-check
-__global__ void __launch_bounds__(WGR) k_msm_flags(const g1a *pks, const uint64_t *rands,
-                                                   const int32_t *pre, const int32_t *pre2,
-                                                   uint32_t n, const uint32_t *seg_off,
-                                                   uint32_t nseg, int32_t *seg_err) {
-  uint32_t i = blockIdx.x * WGR + threadIdx.x;
-  if (i >= n) return;
-  if (aff_is_inf(pks[i]) || rands[i] == 0 || (pre && pre[i] != 0) || (pre2 && pre2[i] != 0))
-    atomicOr(&seg_err[msm_segment(seg_off, nseg, i)], 1);
+// c = 13: lane per (segment, window) t = s * W + w: S_w = A_w + T_w (weights b + 1),
+// affine, paired with -[2^(c w)] g1 at pair n + t
+__global__ void __launch_bounds__(WG) k_msm_wpairs(const g2j *T, const g2j *A, uint32_t nw,
+                                                   uint32_t W, uint32_t n, const uint32_t *seg_off,
+                                                   int empty_is_error, g1s *P, g2a *H,
+                                                   int32_t *seg_err) {
+  uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= nw) return;
+  uint32_t s = t / W, w = t % W;
+  g2j a = A[t], b = T[t];
+  jac_add(a, a, b);
+  g2a o;
+  jac_to_aff(o, a);
+  g1s g;
+  msm_weight(g, k::MSM_W13, w);
+  P[n + t] = g;
+  H[n + t] = o;
+  if (w == 0 && empty_is_error && seg_off[s + 1] == seg_off[s]) atomicOr(&seg_err[s], 1);
 }
 
 // ---------------------------------------------------------------- host side
 // Window widths dividing 65 (64-bit scalars + the signed-digit carry), so that no window
 // is nearly empty (a 2-bit top window would pile every set into two buckets): c = 5
-// (13 windows, 16 buckets each) for segments up to 2^16 sets, else c = 13 (5 windows,
-// 4096 buckets).  Quad gangs below kLaneRegimeSets sets in the launch, one lane per
-// operation above.
+// (13 windows, 16 buckets each, one Miller pair per bucket) for segments up to 2^16 sets,
+// else c = 13 (5 windows of 4096 buckets, per-window trees, one pair per window).  The
+// folds run on quad gangs below kLaneRegimeSets sets in the launch, one lane per
+// addition above.
 MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   uint32_t avg = nseg ? n / nseg : n;
   MsmPlan p;
   p.nseg = nseg;
   p.c = avg >= (1u << 16) ? 13 : 5;
   p.W = 65 / p.c;
+  p.tree = p.c == 13;
+  p.extra = p.tree ? (uint32_t)p.W : ((uint32_t)p.W << (p.c - 1));
   p.quad = n < kLaneRegimeSets;
   p.nb = nseg * ((uint32_t)p.W << (p.c - 1));
   p.max_chunks = (uint32_t)(((uint64_t)p.W * n + MSM_K - 1) / MSM_K) + p.nb;
@@ -320,64 +335,59 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.o_cstart = take((p.nb + 1) * 4);
   p.o_list = take((size_t)p.W * n * 4);
   p.o_chunk = take((size_t)p.max_chunks * sizeof(g2j));
-  p.o_t0 = take((size_t)p.nb * sizeof(g2j));
-  p.o_a0 = take((size_t)p.nb * sizeof(g2j));
-  p.o_t1 = take((size_t)(p.nb / 2 + 1) * sizeof(g2j));
-  p.o_a1 = take((size_t)(p.nb / 2 + 1) * sizeof(g2j));
+  const size_t tn = p.tree ? p.nb : 0;
+  p.o_t0 = take(tn * sizeof(g2j));
+  p.o_a0 = take(tn * sizeof(g2j));
+  p.o_t1 = take((tn / 2 + 1) * sizeof(g2j));
+  p.o_a1 = take((tn / 2 + 1) * sizeof(g2j));
   p.bytes = o;
   return p;
 }
 
-template <bool Q>
-static void launch_msm_points(hipStream_t st, const MsmPlan &p, const g2a *sigs, uint32_t *list,
-                              uint32_t *start, uint32_t *cstart, g2j *chunk, g2j **T, g2j **A,
-                              int &src) {
-  const size_t L = Q ? 4 : 1;
-  k_msm_chunk<Q><<<nblk(L * p.max_chunks), WG, 0, st>>>(sigs, list, start, cstart, p.nb,
-                                                        p.max_chunks, chunk);
-  for (int f = 0; f < p.folds + 1; f++)  // + 1: the digit distribution is not exactly flat
-    k_msm_fold<Q><<<nblk(L * p.max_chunks), WG, 0, st>>>(cstart, p.nb, p.max_chunks, f, chunk);
-  k_msm_bucket<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, T[0], A[0]);
-  src = 0;
-  const uint32_t B = 1u << (p.c - 1), groups = p.nseg * (uint32_t)p.W;
-  for (int l = 0; (1u << (l + 1)) <= B; l++) {
-    uint32_t m = B >> (l + 1);
-    k_msm_tree<Q><<<nblk(L * groups * m), WG, 0, st>>>(T[src], A[src], groups, m, l, T[1 - src],
-                                                       A[1 - src]);
-    src = 1 - src;
-  }
-}
-
 void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
-                const uint64_t *rands, uint32_t n, const uint32_t *seg_off, int empty_is_error,
-                g2a *H, g1s *P, int32_t *seg_err) {
+                const uint64_t *rands, const g1a *pks, const int32_t *pre, const int32_t *pre2,
+                uint32_t n, const uint32_t *seg_off, int empty_is_error, g2a *H, g1s *P,
+                int32_t *seg_err) {
   uint32_t *cnt = reinterpret_cast<uint32_t *>(ws + p.o_cnt);
   uint32_t *start = reinterpret_cast<uint32_t *>(ws + p.o_start);
   uint32_t *cur = reinterpret_cast<uint32_t *>(ws + p.o_cur);
   uint32_t *cstart = reinterpret_cast<uint32_t *>(ws + p.o_cstart);
   uint32_t *list = reinterpret_cast<uint32_t *>(ws + p.o_list);
   g2j *chunk = reinterpret_cast<g2j *>(ws + p.o_chunk);
-  g2j *T[2] = {reinterpret_cast<g2j *>(ws + p.o_t0), reinterpret_cast<g2j *>(ws + p.o_t1)};
-  g2j *A[2] = {reinterpret_cast<g2j *>(ws + p.o_a0), reinterpret_cast<g2j *>(ws + p.o_a1)};
   (void)hipMemsetAsync(cnt, 0, p.nb * 4, st);
   (void)hipMemsetAsync(seg_err, 0, p.nseg * 4, st);
-  k_msm_count<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, cnt);
+  k_msm_count<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, pks, pre,
+                                            pre2, cnt, seg_err);
   k_msm_scan<<<1, 1024, 0, st>>>(cnt, p.nb, start, cur, cstart);
   k_msm_scatter<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, cur,
                                               list);
+  k_msm_chunk<<<nblk(p.max_chunks), WG, 0, st>>>(sigs, list, start, cstart, p.nb, p.max_chunks,
+                                                 chunk);
+  for (int f = 0; f < p.folds + 1; f++) {  // + 1: the digit distribution is not exactly flat
+    if (p.quad)
+      k_msm_fold<true><<<nblk(4 * (size_t)p.max_chunks), WG, 0, st>>>(cstart, p.nb, p.max_chunks,
+                                                                      f, chunk);
+    else
+      k_msm_fold<false><<<nblk(p.max_chunks), WG, 0, st>>>(cstart, p.nb, p.max_chunks, f, chunk);
+  }
+  if (!p.tree) {
+    k_msm_pairs<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, p.extra, n, seg_off,
+                                           empty_is_error, P, H, seg_err);
+    return;
+  }
+  g2j *T[2] = {reinterpret_cast<g2j *>(ws + p.o_t0), reinterpret_cast<g2j *>(ws + p.o_t1)};
+  g2j *A[2] = {reinterpret_cast<g2j *>(ws + p.o_a0), reinterpret_cast<g2j *>(ws + p.o_a1)};
+  k_msm_bucket<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, T[0], A[0]);
   int src = 0;
-  if (p.quad)
-    launch_msm_points<true>(st, p, sigs, list, start, cstart, chunk, T, A, src);
-  else
-    launch_msm_points<false>(st, p, sigs, list, start, cstart, chunk, T, A, src);
-  k_msm_final<<<nblk(4 * (size_t)p.nseg), WG, 0, st>>>(T[src], A[src], p.nseg, p.W, p.c, n,
-                                                       seg_off, empty_is_error, P, H, seg_err);
-}
-
-void launch_msm_flags(hipStream_t st, const g1a *pks, const uint64_t *rands, const int32_t *pre,
-                      const int32_t *pre2, uint32_t n, const uint32_t *seg_off, uint32_t nseg,
-                      int32_t *seg_err) {
-  if (n) k_msm_flags<<<nblk(n, WGR), WGR, 0, st>>>(pks, rands, pre, pre2, n, seg_off, nseg, seg_err);
+  const uint32_t B = 1u << (p.c - 1), groups = p.nseg * (uint32_t)p.W;
+  for (int l = 0; (1u << (l + 1)) <= B; l++) {
+    uint32_t m = B >> (l + 1);
+    k_msm_tree<<<nblk((size_t)groups * m), WG, 0, st>>>(T[src], A[src], groups, m, l, T[1 - src],
+                                                         A[1 - src]);
+    src = 1 - src;
+  }
+  k_msm_wpairs<<<nblk(groups), WG, 0, st>>>(T[src], A[src], groups, (uint32_t)p.W, n, seg_off,
+                                            empty_is_error, P, H, seg_err);
 }
 
 }  // namespace gbls
