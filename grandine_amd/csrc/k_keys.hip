@@ -120,6 +120,68 @@ __global__ void __launch_bounds__(WG) k_g1_gather_idx(const g1a *reg, uint32_t n
   st[i] = v < nreg ? ST_SUCCESS : ST_BAD_ENCODING;
 }
 
+// ---------------------------------------------------------------- row aggregation
+// Many segments (committees, sync-committee messages): one DPP row (16 lanes) per
+// segment instead of a 256-lane workgroup.  Each lane sums every 16th key with mixed
+// additions, the row folds its 16 partial sums in 4 row_shl steps (VALU moves, no LDS,
+// no barrier), and the row's lane 0 converts to affine: four segments per wave share
+// one inversion's latency, where the workgroup form spends a tree of 8 LDS levels and a
+// whole inversion per segment.
+template <int K>
+__device__ __forceinline__ uint32_t row_shl(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + K, 0xf, 0xf, true);
+}
+template <int K, class F>
+__device__ __forceinline__ void jac_row_fold(jac<F> &acc, uint32_t &flag) {
+  jac<F> o;
+  uint32_t *d = reinterpret_cast<uint32_t *>(&o);
+  const uint32_t *a = reinterpret_cast<const uint32_t *>(&acc);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(jac<F>) / 4); i++) d[i] = row_shl<K>(a[i]);
+  flag |= row_shl<K>(flag);
+  jac_add(acc, acc, o);  // lanes past the row end read zeros: infinity
+}
+// segment s = sum of pts[i] (idx == nullptr) or reg[idx[i]], i in [off[s], off[s+1])
+template <class F>
+__global__ void __launch_bounds__(WG) k_aggregate_rows(const aff<F> *pts, uint32_t nreg,
+                                                       const uint32_t *idx, const uint32_t *off,
+                                                       uint32_t nseg, aff<F> *out, int32_t *st) {
+  uint32_t t = blockIdx.x * WG + threadIdx.x;
+  uint32_t s = t >> 4, r = t & 15;
+  if (s >= nseg) return;  // whole rows
+  uint32_t b = off[s], e = off[s + 1];
+  jac<F> acc;
+  jac_set_inf(acc);
+  uint32_t oob = 0;
+  for (uint32_t i = b + r; i < e; i += 16) {
+    uint32_t v = idx ? idx[i] : i;
+    if (idx && v >= nreg)
+      oob = 1;
+    else
+      jac_add_aff(acc, acc, pts[v]);
+  }
+  jac_row_fold<1>(acc, oob);
+  jac_row_fold<2>(acc, oob);
+  jac_row_fold<4>(acc, oob);
+  jac_row_fold<8>(acc, oob);
+  if (r != 0) return;
+  aff<F> o;
+  jac_to_aff(o, acc);
+  int32_t status = ST_SUCCESS;
+  if (e == b)
+    status = ST_AGGR_TYPE_MISMATCH;
+  else if (oob)
+    status = ST_BAD_ENCODING;
+  if (idx && status != ST_SUCCESS) {
+    f_zero(o.x);
+    f_zero(o.y);
+  }
+  out[s] = o;
+  if (st) st[s] = status;
+}
+// rows for many segments; the 256-lane workgroup form for a few long ones
+constexpr uint32_t kRowAggregateMinSegs = 128;
+
 // ---------------------------------------------------------------- key material (a15)
 HD void scalar_from_be32(uint32_t (&s)[8], const uint8_t *b) {
   for (int i = 0; i < 8; i++) {
@@ -188,15 +250,27 @@ __global__ void __launch_bounds__(256) k_mad_peak(uint64_t *sink, uint32_t iters
 // ---------------------------------------------------------------- launchers
 void launch_g1_aggregate_seg(hipStream_t st, const g1a *pks, const uint32_t *off, uint32_t nseg,
                              g1a *out, int32_t *status) {
-  if (nseg) k_g1_aggregate_seg<<<nseg, WGR, 0, st>>>(pks, off, nseg, out, status);
+  if (nseg >= kRowAggregateMinSegs)
+    k_aggregate_rows<fp><<<nblk(16 * (size_t)nseg), WG, 0, st>>>(pks, 0, nullptr, off, nseg, out,
+                                                                 status);
+  else if (nseg)
+    k_g1_aggregate_seg<<<nseg, WGR, 0, st>>>(pks, off, nseg, out, status);
 }
 void launch_g2_aggregate_seg(hipStream_t st, const g2a *pts, const uint32_t *off, uint32_t nseg,
                              g2a *out, int32_t *status) {
-  if (nseg) k_g2_aggregate_seg<<<nseg, WGR, 0, st>>>(pts, off, nseg, out, status);
+  if (nseg >= kRowAggregateMinSegs)
+    k_aggregate_rows<fp2><<<nblk(16 * (size_t)nseg), WG, 0, st>>>(pts, 0, nullptr, off, nseg, out,
+                                                                  status);
+  else if (nseg)
+    k_g2_aggregate_seg<<<nseg, WGR, 0, st>>>(pts, off, nseg, out, status);
 }
 void launch_g1_aggregate_idx(hipStream_t st, const g1a *reg, uint32_t nreg, const uint32_t *idx,
                              const uint32_t *off, uint32_t nseg, g1a *out, int32_t *status) {
-  if (nseg) k_g1_aggregate_idx<<<nseg, WGR, 0, st>>>(reg, nreg, idx, off, nseg, out, status);
+  if (nseg >= kRowAggregateMinSegs)
+    k_aggregate_rows<fp><<<nblk(16 * (size_t)nseg), WG, 0, st>>>(reg, nreg, idx, off, nseg, out,
+                                                                 status);
+  else if (nseg)
+    k_g1_aggregate_idx<<<nseg, WGR, 0, st>>>(reg, nreg, idx, off, nseg, out, status);
 }
 void launch_g1_gather_idx(hipStream_t st, const g1a *reg, uint32_t nreg, const uint32_t *idx,
                           uint32_t n, g1a *out, int32_t *status) {

@@ -183,6 +183,74 @@ def test_aggregate_segments_api(L, G, B):
             assert B.PublicKey(out.raw[96 * i:96 * i + 96]).to_bytes().hex() == c["out"]
 
 
+def test_aggregate_segments_rows(L, G, B):
+    """>= 128 segments take the row-per-segment kernel (k_aggregate_rows): the golden
+    G1 / G2 aggregation cases repeated 64 times, and registry indices (out-of-range and
+    empty segments included), against the golden outputs and the 256-lane form."""
+    a = gold("aggregate")
+    reps = 64
+    keys, off, want = [], [0], []
+    for _ in range(reps):
+        for c in a["g1"]:
+            keys += [_pk(B, h).raw for h in c["pks"]]
+            off.append(len(keys))
+            want.append(c)
+    n = len(want)
+    assert n >= 128
+    out = ctypes.create_string_buffer(96 * n)
+    st = G.i32_array(n)
+    G.check(L.gbls_g1_aggregate_segments(G.buf(b"".join(keys)), G.u32_array(off), n, out, st), "rows g1")
+    for i, c in enumerate(want):
+        assert st[i] == c["status"]
+        if c["status"] == 0:
+            assert B.PublicKey(out.raw[96 * i:96 * i + 96]).to_bytes().hex() == c["out"]
+    # G2
+    sigs, off2, want2 = [], [0], []
+    for _ in range(reps):
+        for c in a["g2"]:
+            sigs += [_sig(B, h).raw for h in c["sigs"]]
+            off2.append(len(sigs))
+            want2.append(c["out"])
+    m = len(want2)
+    assert m >= 128
+    out2 = ctypes.create_string_buffer(192 * m)
+    st2 = G.i32_array(m)
+    G.check(L.gbls_g2_aggregate_segments(G.buf(b"".join(sigs)), G.u32_array(off2), m, out2, st2), "rows g2")
+    for i, h in enumerate(want2):
+        assert st2[i] == 0
+        assert B.Signature(out2.raw[192 * i:192 * i + 192]).to_bytes().hex() == h
+    # registry indices: row kernel vs the workgroup kernel (few segments) on the same data
+    from grandine_amd import factory as F
+    nreg = 4096
+    _, comp = F.registry(nreg, seed=b"rows")
+    assert not F.load_registry(comp).any()
+    import numpy as np
+    rng = np.random.default_rng(7)
+    sizes = rng.integers(0, 40, size=300)
+    sizes[5] = 0
+    idx = rng.integers(0, nreg, size=int(sizes.sum()), dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    idx[int(offs[9])] = nreg + 3  # out of range in segment 9 (sizes[9] > 0 checked below)
+    assert sizes[9] > 0
+    ns = len(sizes)
+    o_rows = ctypes.create_string_buffer(96 * ns)
+    s_rows = G.i32_array(ns)
+    G.check(L.gbls_g1_aggregate_indexed(idx.ctypes.data_as(ctypes.c_void_p), offs.ctypes.data_as(ctypes.c_void_p),
+                                        ns, o_rows, s_rows), "rows idx")
+    for k in range(0, ns, 100):  # the same segments, 100 at a time: workgroup kernel
+        cnt = min(100, ns - k)
+        sub_off = (offs[k:k + cnt + 1] - offs[k]).astype(np.uint32)
+        sub_idx = np.ascontiguousarray(idx[offs[k]:offs[k + cnt]])
+        o_wg = ctypes.create_string_buffer(96 * cnt)
+        s_wg = G.i32_array(cnt)
+        G.check(L.gbls_g1_aggregate_indexed(sub_idx.ctypes.data_as(ctypes.c_void_p),
+                                            sub_off.ctypes.data_as(ctypes.c_void_p), cnt, o_wg, s_wg), "wg idx")
+        for j in range(cnt):
+            assert s_rows[k + j] == s_wg[j], k + j
+            assert o_rows.raw[96 * (k + j):96 * (k + j + 1)] == o_wg.raw[96 * j:96 * (j + 1)], k + j
+    assert s_rows[5] == G.AGGR_TYPE_MISMATCH and s_rows[9] == G.BAD_ENCODING
+
+
 # ------------------------------------------------------------------ verdicts
 def test_verify_cases(B):
     for c in gold("verify")["cases"]:
