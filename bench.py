@@ -400,14 +400,17 @@ def main():
     ns = L.gbls_profile_read(ms, calls, nst)
     stages = {L.gbls_stage_name(i).decode(): (ms[i], calls[i]) for i in range(ns) if calls[i]}
     peak = L.gbls_measure_mad64_peak()
-    # dominant kernel: the longest stage with algorithmic work of its own (k_lines_S, the
-    # extra pairs' lines, mostly waits for SIMDs held by the main stream)
-    cand = [k for k in stages if W_FPMUL.get(k, 0) > 0 and k != "k_lines_S"]
+    # dominant kernel: the longest single-kernel stage with algorithmic work of its own
+    # (rocprofv3 reports the same kernel's duration).  Not roofline rows: the multi-kernel
+    # stages k_msm / k_ml_reduce / k_g2sum, and k_lines_S, which mostly waits for SIMDs
+    # held by the main stream.
+    multi = {"k_msm", "k_ml_reduce", "k_g2sum", "k_lines_S"}
+    cand = [k for k in stages if W_FPMUL.get(k, 0) > 0 and k not in multi]
     dom = max(cand, key=lambda k: stages[k][0]) if cand else None
     roof = None
     if dom:
         tot_ms, ncalls = stages[dom]
-        avg_s = tot_ms / ncalls * 1e-3
+        avg_s = tot_ms / args.steps * 1e-3  # the stage's time per step (one or more launches)
         mads = leg.stage_units(dom) * W_FPMUL.get(dom, 0) * MAD_PER_FPMUL
         ach = mads / avg_s / 1e12
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4),

@@ -309,6 +309,36 @@ HD void lines_of(uint32_t *L, uint32_t np, uint32_t pair, const g2a &Q) {
   }
 }
 
+// Lines of events [e0, e1) of Q, stored at event index e - e0 (an event-range slice of
+// lines_of).  T carries the running point between slices: read when e0 > 0, written
+// when e1 < ML_EVENTS (Ts may be null for the full range).
+HD void lines_range(uint32_t *L, uint32_t np, uint32_t pair, const g2a &Q, int e0, int e1, g2h *Ts) {
+  fp2 L0, L2, L3;
+  if (aff_is_inf(Q)) {
+    fp2_one(L0);
+    fp2_zero(L2);
+    fp2_zero(L3);
+    for (int e = e0; e < e1; e++) line_put(L, np, pair, e - e0, L0, L2, L3);
+    return;
+  }
+  g2h T;
+  if (e0 > 0) {
+    T = Ts[pair];
+  } else {
+    T.x = Q.x;
+    T.y = Q.y;
+    fp2_one(T.z);
+  }
+  for (int e = e0; e < e1; e++) {
+    if (ev_is_dbl(e))
+      line_dbl(T, L0, L2, L3);
+    else
+      line_add_aff(T, Q, L0, L2, L3);
+    line_put(L, np, pair, e - e0, L0, L2, L3);
+  }
+  if (e1 < ML_EVENTS) Ts[pair] = T;
+}
+
 // Reference single-pair Miller loop (host harness): f_{|x|,Q}(P), conjugated (x < 0).
 HD void miller_loop_aff(fp12 &f, const g1a &P, const g2a &Q) {
   fp12_one(f);

@@ -132,7 +132,7 @@ struct Ctx {
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
-  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, gpart, lines, V0, V1, tab, part, err, out0,
+  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, gpart, lines, Ts, V0, V1, tab, part, err, out0,
       out1, pks, pre, pre2, msm;
   void *stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
@@ -421,10 +421,19 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   //   [pair list][groups][g2 chunks][seg_chunk][reduction levels][seg_off]
   // Level 0 of the Miller product: per segment, its pairs (sets, then the extra pairs)
   // in groups of <= G, strided so that a wave's lanes read adjacent pairs (k_ml_group).
+  // Line buffer: all 68 events of every pair when that fits kLineBudget, else event
+  // slices of EC events, generated and consumed one slice at a time after the join (the
+  // running points T in HBM between slices), so that memory stays bounded at C5 scale.
+  const size_t event_bytes = (size_t)np * 72 * 4;
+  int EC = ML_EVENTS;
+  if (event_bytes * ML_EVENTS > kLineBudget)
+    EC = (int)std::max<size_t>(1, kLineBudget / event_bytes);
+  const bool sliced = EC < ML_EVENTS;
+  const size_t line_words = (size_t)np * EC * 72;
   // G: the largest power of two <= 64 that still gives >= 65536 lanes (one wave per
-  // SIMD) over the 68 events.
+  // SIMD) per group launch (EC events).
   uint32_t G = 1;
-  while (G < 64 && (uint64_t)ML_EVENTS * np / (2 * G) >= 65536) G *= 2;
+  while (G < 64 && (uint64_t)EC * np / (2 * G) >= 65536) G *= 2;
   std::vector<uint32_t> &tab = c.host_tab;
   tab.clear();
   tab.resize(np);
@@ -499,10 +508,10 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   const size_t segoff_at = tab.size();
   tab.insert(tab.end(), seg_off, seg_off + nseg + 1);
   // ---- workspaces
-  const size_t line_words = (size_t)np * ML_EVENTS * 72;
   size_t v1_n = 1, v0_n = ngroup;
   for (size_t l = 0; l < levels.size(); l++)
     (l & 1 ? v0_n : v1_n) = std::max(l & 1 ? v0_n : v1_n, levels[l].nout);
+  if (sliced && !c.ensure(c.Ts, np * sizeof(g2h))) return false;
   if (sig_groupcheck && !c.ensure(c.pre2, n * sizeof(int32_t) + 16)) return false;
   if (!c.ensure(c.U, 2 * n * sizeof(fp2) + 16) || !c.ensure(c.Q, 2 * n * sizeof(g2j) + 16) ||
       !c.ensure(c.H, np * sizeof(g2a)) || !c.ensure(c.P, np * sizeof(g1s)) ||
@@ -552,9 +561,10 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
                    T + segoff_at, NS, N, pks, rands, pre, pre2, empty_is_error, gpart, gpart_err,
                    c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
   }
-  {
+  if (!sliced) {
     StageTimer t(S_LINES_S, c.side2);
-    launch_lines(c.side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, c.lines.as<uint32_t>());
+    launch_lines(c.side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, ML_EVENTS, nullptr,
+                 c.lines.as<uint32_t>());
   }
   {
     StageTimer t(S_H2C_FIELD, st);
@@ -568,18 +578,23 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     StageTimer t(S_H2C_CLEAR, st);
     launch_h2c_clear(st, c.Q.as<g2j>(), N, c.H.as<g2a>());
   }
-  {
+  if (!sliced) {
     StageTimer t(S_LINES, st);
-    launch_lines(st, c.H.as<g2a>(), 0, N, NP, c.lines.as<uint32_t>());
+    launch_lines(st, c.H.as<g2a>(), 0, N, NP, 0, ML_EVENTS, nullptr, c.lines.as<uint32_t>());
   }
   HIPCHK(hipEventRecord(c.ev_side1, c.side1));
   HIPCHK(hipEventRecord(c.ev_side2, c.side2));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side1, 0));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
-  {
+  for (int e0 = 0; e0 < ML_EVENTS; e0 += EC) {
+    const int e1 = std::min(ML_EVENTS, e0 + EC);
+    if (sliced) {
+      StageTimer t(S_LINES, st);
+      launch_lines(st, c.H.as<g2a>(), 0, NP, NP, e0, e1, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
+    }
     StageTimer t(S_ML_LEAF, st);
     launch_ml_group(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T, T + grp_off,
-                    (uint32_t)ngroup, c.V0.as<fp12>());
+                    (uint32_t)ngroup, e0, e1, c.V0.as<fp12>());
   }
   fp12 *cur = c.V0.as<fp12>(), *other = c.V1.as<fp12>();
   {

@@ -16,6 +16,8 @@ constexpr uint32_t NONE = 0xffffffffu;
 // Launches of at least this many sets fill every SIMD with lane-per-set work, so stages
 // with a quad-gang (latency) and a lane-per-set (throughput) variant pick the latter.
 constexpr uint32_t kLaneRegimeSets = 32768;
+// line-coefficient buffer bound: above it the Miller lines are made in event slices
+constexpr size_t kLineBudget = (size_t)1 << 30;
 
 inline unsigned nblk(size_t n, unsigned per = WG) { return (unsigned)((n + per - 1) / per); }
 
@@ -85,14 +87,17 @@ void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
                 int32_t *seg_err);
 
 // k_lines.hip -- Miller-loop line functions of every pair
-// lines of pairs [first, first + count) of np (H indexed by pair)
+// lines of events [e0, e1) of pairs [first, first + count) of np (H indexed by pair),
+// stored at event e - e0; Ts: the running point between event slices (null: full range)
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
-                  uint32_t *lines);
+                  int e0, int e1, g2h *Ts, uint32_t *lines);
 
 // k_miller.hip -- Miller product tree + Horner
 // groups: (first index into plist, stride, count) per group, segment by segment
+// events [e0, e1): lines at event e - e0, products to V0[e * ngroup + g]
 void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
-                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, fp12 *V0);
+                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
+                     int e1, fp12 *V0);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);
 void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial);

@@ -22,24 +22,25 @@ __device__ __forceinline__ void ml_eval(sp034 &s, const uint32_t *L, uint32_t np
   line_eval_s(s, L0, L2, L3, Pp);
 }
 
-// grid (ceil(ngroup / 64), 68); group g = (first plist index, stride, count)
+// grid (ceil(ngroup / 64), e1 - e0); group g = (first plist index, stride, count); the
+// lines buffer holds events [e0, e1) at e - e0
 __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np, const g1s *P,
                                                  const uint32_t *plist, const uint32_t *grp,
-                                                 uint32_t ngroup, fp12 *V0) {
+                                                 uint32_t ngroup, int e0, fp12 *V0) {
   uint32_t g = blockIdx.x * WG + threadIdx.x;
-  int e = blockIdx.y;
+  int el = blockIdx.y, e = e0 + el;
   if (g >= ngroup) return;
   uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
   sp034 sa, sb;
   fp12 acc;
-  ml_eval(sa, L, np, P, plist[at], e);
+  ml_eval(sa, L, np, P, plist[at], el);
   if (cnt == 1) {
     sp_to_fp12(acc, sa);
   } else {
-    ml_eval(sb, L, np, P, plist[at + stride], e);
+    ml_eval(sb, L, np, P, plist[at + stride], el);
     sp_mul_sp(acc, sa, sb);
     for (uint32_t j = 2; j < cnt; j++) {
-      ml_eval(sa, L, np, P, plist[at + j * stride], e);
+      ml_eval(sa, L, np, P, plist[at + j * stride], el);
       fp12_mul_034(acc, acc, sa);
     }
   }
@@ -92,9 +93,10 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
 }
 
 void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
-                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, fp12 *V0) {
-  dim3 grid(nblk(ngroup), ML_EVENTS);
-  if (ngroup) k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, V0);
+                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
+                     int e1, fp12 *V0) {
+  dim3 grid(nblk(ngroup), e1 - e0);
+  if (ngroup && e1 > e0) k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
 }
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout) {
