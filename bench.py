@@ -85,19 +85,18 @@ def cpu_threads():
     return max(1, n)
 
 
-def pmc_traffic(kernel, n):
+def pmc_traffic(kernel, default_cmd):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
-    summary of the default command (profiles/<round>/pmc_bytes.csv, tools/prof/pmc_bytes.py;
-    FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
-    for rnd in ("r02", "r01"):
-        path = os.path.join(ROOT, "profiles", rnd, "pmc_bytes.csv")
-        if n != 4096 or not os.path.exists(path):
-            continue
-        with open(path) as f:
-            for row in f.read().splitlines()[1:]:
-                cols = row.split(",")
-                if cols[0].split("::")[-1] == kernel:
-                    return float(cols[4])
+    summary of the default command (profiles/r02/pmc_bytes.csv, tools/prof/pmc_bytes.py;
+    FETCH_SIZE doubled per the gfx950 correction).  None for other commands or if absent."""
+    path = os.path.join(ROOT, "profiles", "r02", "pmc_bytes.csv")
+    if not default_cmd or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        for row in f.read().splitlines()[1:]:
+            cols = row.split(",")
+            if cols[0].split("::")[-1] == kernel:
+                return float(cols[4])
     return None
 
 
@@ -416,7 +415,8 @@ def main():
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4),
                 "peak": round(peak / 1e12, 3), "unit": "Tmad64/s",
                 "frac": round(ach / (peak / 1e12), 5) if peak else None,
-                "traffic": pmc_traffic(dom, leg.units) if cfg == "C2" else None,
+                "traffic": pmc_traffic(dom, cfg == "C2" and args.sets in (0, 4096) and args.batches == 4
+                                       and args.inflight == 1),
                 "avg_launch_ms": round(tot_ms / ncalls, 4),
                 "path": {"fpmul_per_step": leg.path_fpmul(),
                          "achieved": round(leg.path_fpmul() * MAD_PER_FPMUL * args.steps / dt / 1e12, 4),
