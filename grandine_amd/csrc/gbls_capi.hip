@@ -422,8 +422,9 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   // Level 0 of the Miller product: per segment, its pairs (sets, then the extra pairs)
   // in groups of <= G, strided so that a wave's lanes read adjacent pairs (k_ml_group).
   // Line buffer: all 68 events of every pair when that fits kLineBudget, else event
-  // slices of EC events, generated and consumed one slice at a time after the join (the
-  // running points T in HBM between slices), so that memory stays bounded at C5 scale.
+  // slices of EC events (the running points T in HBM between slices), so that memory stays
+  // bounded at C5 scale.  The first slice is generated before the join like the unsliced
+  // lines (sets on the main stream, extra pairs on side 2), later ones after it.
   const size_t event_bytes = (size_t)np * 72 * 4;
   int EC = ML_EVENTS;
   if (event_bytes * ML_EVENTS > kLineBudget)
@@ -561,9 +562,9 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
                    T + segoff_at, NS, N, pks, rands, pre, pre2, empty_is_error, gpart, gpart_err,
                    c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
   }
-  if (!sliced) {
+  {  // the extra pairs' lines of the first event slice (all events when not sliced)
     StageTimer t(S_LINES_S, c.side2);
-    launch_lines(c.side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, ML_EVENTS, nullptr,
+    launch_lines(c.side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, EC, c.Ts.as<g2h>(),
                  c.lines.as<uint32_t>());
   }
   {
@@ -578,9 +579,9 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     StageTimer t(S_H2C_CLEAR, st);
     launch_h2c_clear(st, c.Q.as<g2j>(), N, c.H.as<g2a>());
   }
-  if (!sliced) {
+  {  // the sets' lines of the first event slice, before the join
     StageTimer t(S_LINES, st);
-    launch_lines(st, c.H.as<g2a>(), 0, N, NP, 0, ML_EVENTS, nullptr, c.lines.as<uint32_t>());
+    launch_lines(st, c.H.as<g2a>(), 0, N, NP, 0, EC, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
   }
   HIPCHK(hipEventRecord(c.ev_side1, c.side1));
   HIPCHK(hipEventRecord(c.ev_side2, c.side2));
@@ -588,7 +589,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
   for (int e0 = 0; e0 < ML_EVENTS; e0 += EC) {
     const int e1 = std::min(ML_EVENTS, e0 + EC);
-    if (sliced) {
+    if (e0 > 0) {  // later slices: every pair, after the join
       StageTimer t(S_LINES, st);
       launch_lines(st, c.H.as<g2a>(), 0, NP, NP, e0, e1, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
     }

@@ -13,9 +13,13 @@ namespace gbls {
 constexpr int WG = 64;    // per-lane kernels: one wave per workgroup
 constexpr int WGR = 256;  // segment reductions: 4 waves, LDS tree
 constexpr uint32_t NONE = 0xffffffffu;
-// Launches of at least this many sets fill every SIMD with lane-per-set work, so stages
-// with a quad-gang (latency) and a lane-per-set (throughput) variant pick the latter.
-constexpr uint32_t kLaneRegimeSets = 32768;
+// Stages with a quad-gang (latency) and a lane-per-item (throughput) variant pick the
+// latter from these launch sizes on (measured on MI355X, 12 x 4096-set C2 step: Miller lines
+// 3.32 ms quad vs 2.44 ms lane at 49152 pairs; cofactor clearing 4.99 vs 4.40 ms at 32768
+// sets, the other streams filling the SIMDs a lane launch leaves free).
+constexpr uint32_t kLaneRegimeSets = 32768;   // G1 products, MSM folds
+constexpr uint32_t kLaneRegimeClear = 32768;  // cofactor clearing
+constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
 // line-coefficient buffer bound: above it the Miller lines are made in event slices
 constexpr size_t kLineBudget = (size_t)1 << 30;
 

@@ -3,7 +3,7 @@
 // One DPP quad (4 lanes) per message: the doublings and additions run quad-cooperatively
 // (bls_gang.h); psi and the affine conversion run
 // redundantly in all four lanes and lane 0 stores.  Output: affine points (Miller-loop
-// input).  Launches of at least kLaneRegimeSets messages run one message per lane
+// input).  Launches of at least kLaneRegimeClear messages run one message per lane
 // (k_h2c_clear_lane: a quarter of the instructions per message, the chip already full).
 #include "gbls_common.h"
 #include "bls_gang.h"
@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n,
 
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   if (!n) return;
-  if (n >= kLaneRegimeSets)
+  if (n >= kLaneRegimeClear)
     k_h2c_clear_lane<<<nblk(n), WG, 0, st>>>(Q, n, H);
   else
     k_h2c_clear<<<nblk((size_t)n * 4), WG, 0, st>>>(Q, n, H);

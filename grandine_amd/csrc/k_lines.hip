@@ -5,7 +5,7 @@
 // gang_line_add_aff); lane q stores line components c with c % 4 == q.  Large batches
 // generate and consume the lines in event slices (the running point T kept in HBM
 // between slices), so the buffer holds a slice of events, not all 68.  Launches of at
-// least kLaneRegimeSets pairs run one pair per lane instead (k_lines_lane).
+// least kLaneRegimeLines pairs run one pair per lane instead (k_lines_lane).
 #include "gbls_common.h"
 #define GBLS_GANG_LINES
 #include "bls_gang.h"
@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first,
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
                   int e0, int e1, g2h *Ts, uint32_t *lines) {
   if (!count) return;
-  if (count >= kLaneRegimeSets)
+  if (count >= kLaneRegimeLines)
     k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
   else
     k_lines<<<nblk((size_t)count * 4), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
