@@ -126,7 +126,7 @@ struct Ctx {
   int hipdev = -1;
   hipStream_t own = nullptr, side1 = nullptr, side2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
-             ev_done = nullptr, ev_upl = nullptr;
+             ev_done = nullptr, ev_upl = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool done_pending = false, upl_pending = false;
   bool active = false;                // a call holds the lease and has begun
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
@@ -141,13 +141,19 @@ struct Ctx {
   bool init(int dev) {
     hipdev = dev;
     HIPCHK(hipSetDevice(dev));
-    HIPCHK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&side1, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&side2, hipStreamNonBlocking));
+    // the hash_to_G2 -> lines chain is the critical path: its stream gets the highest
+    // priority, the key-side and signature-side streams (slack of several ms) the lowest
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(hipStreamCreateWithPriority(&own, hipStreamNonBlocking, greatest));
+    HIPCHK(hipStreamCreateWithPriority(&side1, hipStreamNonBlocking, least));
+    HIPCHK(hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, least));
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side1, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side2, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_pks, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_upl, hipEventDisableTiming));
     return true;
@@ -402,7 +408,16 @@ bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t s
 bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *msg_off,
                        const g2a *sigs, const PkSource &src, const uint64_t *rands,
                        bool sig_groupcheck, size_t n, const uint32_t *seg_off, size_t nseg,
-                       int empty_is_error, fp12 *partials, int32_t *seg_err, hipStream_t st) {
+                       int empty_is_error, fp12 *partials, int32_t *seg_err,
+                       hipStream_t caller) {
+  // The main chain runs on the context's high-priority stream; a caller stream (device
+  // entry points) hands over to it and waits for it at the end.
+  hipStream_t st = caller;
+  if (caller != c.own) {
+    HIPCHK(hipEventRecord(c.ev_in, caller));
+    HIPCHK(hipStreamWaitEvent(c.own, c.ev_in, 0));
+    st = c.own;
+  }
   bool single = !rands && n == nseg;  // one set per segment, r = 1
   for (size_t s = 0; single && s <= nseg; s++) single = seg_off[s] == s;
   // bucket MSM for S when every segment is large (segment sizes >= msm_min)
@@ -530,6 +545,15 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   HIPCHK(hipEventRecord(c.ev_fork, st));
   HIPCHK(hipStreamWaitEvent(c.side1, c.ev_fork, 0));
   HIPCHK(hipStreamWaitEvent(c.side2, c.ev_fork, 0));
+  // main stream first: its first kernels reach the GPU before the side streams' floods
+  {
+    StageTimer t(S_H2C_FIELD, st);
+    launch_h2c_field(st, msgs, msg_off, N, nullptr, 0, c.U.as<fp2>());
+  }
+  {
+    StageTimer t(S_H2C_MAP, st);
+    launch_h2c_map(st, c.U.as<fp2>(), 2 * N, c.Q.as<g2j>());
+  }
   const g1a *pks = nullptr;
   const int32_t *pre = nullptr;
   if (!resolve_pks(c, d, src, n, c.side1, &pks, &pre)) return false;
@@ -568,14 +592,6 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
                  c.lines.as<uint32_t>());
   }
   {
-    StageTimer t(S_H2C_FIELD, st);
-    launch_h2c_field(st, msgs, msg_off, N, nullptr, 0, c.U.as<fp2>());
-  }
-  {
-    StageTimer t(S_H2C_MAP, st);
-    launch_h2c_map(st, c.U.as<fp2>(), 2 * N, c.Q.as<g2j>());
-  }
-  {
     StageTimer t(S_H2C_CLEAR, st);
     launch_h2c_clear(st, c.Q.as<g2j>(), N, c.H.as<g2a>());
   }
@@ -608,6 +624,10 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   {
     StageTimer t(S_ML_HORNER, st);
     launch_ml_horner(st, cur, NS, partials);
+  }
+  if (st != caller) {
+    HIPCHK(hipEventRecord(c.ev_out, st));
+    HIPCHK(hipStreamWaitEvent(caller, c.ev_out, 0));
   }
   HIPCHK(hipGetLastError());
   return true;
