@@ -43,8 +43,8 @@ __device__ __forceinline__ void fp_quad_bcast(fp &r, const fp &a) {
 __device__ __forceinline__ void gang_fp2_mul(fp2 &r, const fp2 &a, const fp2 &b, int q) {
   fp x, y, p, t0, t1, t2;
   fp sa, sb;
-  fp_add(sa, a.c0, a.c1);
-  fp_add(sb, b.c0, b.c1);
+  fp_add_lazy(sa, a.c0, a.c1);  // < 2p: a Montgomery operand
+  fp_add_lazy(sb, b.c0, b.c1);
 #pragma unroll
   for (int i = 0; i < 12; i++) {
     x.l[i] = q == 0 ? a.c0.l[i] : (q == 1 ? a.c1.l[i] : sa.l[i]);
