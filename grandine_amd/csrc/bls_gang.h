@@ -292,6 +292,60 @@ __device__ __forceinline__ void gang1_add(g1j &r, const g1j &a, const g1j &b, in
   fp_sub(r.y, t, S1);        // Y3 = R (V - X3) - 2 S1 J
 }
 
+// ---------------------------------------------------------------- 16-lane row gangs
+// For small launches (a lone 4096-set batch fills 256 of 1024 SIMDs with quads): one DPP
+// row (16 lanes) per pair in the Miller-line kernel.  Each dependency level issues up to
+// four Fp2 products at once, quad j of the row computing product j as three Karatsuba Fp
+// products (lanes k = 0, 1, 2; lane 3 repeats 2), so a level costs ONE Fp product of
+// latency: Miller doubling step 3 levels (quad: 7 products), addition step 4 (quad: 12).
+// Products are recombined inside the quad (quad_perm), then shared with the row by
+// row_newbcast: VALU moves, no LDS.  Every lane ends holding the same values.  (Row
+// doublings / additions for cofactor clearing measured slower than the quad ones: 2.01 vs
+// 1.91 ms at 4096 sets, the selects and broadcasts outweighing 3 vs 5 product levels.)
+template <int L>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + L, 0xf, 0xf, false);
+}
+template <int L>
+__device__ __forceinline__ void fp2_row_bcast(fp2 &r, const fp2 &a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = row_bcast<L>(a.c0.l[i]);
+    r.c1.l[i] = row_bcast<L>(a.c1.l[i]);
+  }
+}
+// R_j = A_j B_j (j < 4) in every lane of the row; l = lane & 15.  R may alias inputs.
+__device__ __forceinline__ void row_mul4(fp2 &R0, fp2 &R1, fp2 &R2, fp2 &R3, const fp2 &A0,
+                                         const fp2 &A1, const fp2 &A2, const fp2 &A3,
+                                         const fp2 &B0, const fp2 &B1, const fp2 &B2,
+                                         const fp2 &B3, int l) {
+  const int j = l >> 2, k = l & 3;
+  fp2 a, b;
+  fp2_sel4(a, j, A0, A1, A2, A3);
+  fp2_sel4(b, j, B0, B1, B2, B3);
+  fp x, y, sa, sb;
+  fp_add_lazy(sa, a.c0, a.c1);  // < 2p: a Montgomery operand
+  fp_add_lazy(sb, b.c0, b.c1);
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    x.l[i] = k == 0 ? a.c0.l[i] : (k == 1 ? a.c1.l[i] : sa.l[i]);
+    y.l[i] = k == 0 ? b.c0.l[i] : (k == 1 ? b.c1.l[i] : sb.l[i]);
+  }
+  fp p, t0, t1, t2;
+  fp_mul(p, x, y);
+  fp_quad_bcast<0>(t0, p);
+  fp_quad_bcast<1>(t1, p);
+  fp_quad_bcast<2>(t2, p);
+  fp2 c;
+  fp_sub(c.c0, t0, t1);
+  fp_add(t0, t0, t1);
+  fp_sub(c.c1, t2, t0);
+  fp2_row_bcast<0>(R0, c);
+  fp2_row_bcast<4>(R1, c);
+  fp2_row_bcast<8>(R2, c);
+  fp2_row_bcast<12>(R3, c);
+}
+
 // [|x|]P with quad-cooperative doublings and additions
 __device__ __forceinline__ void gang_mul_by_xabs(g2j &r, const g2j &p, int q) {
   g2j acc = p;
@@ -396,6 +450,58 @@ __device__ __forceinline__ void gang_line_add_aff(g2h &T, const g2a &Q, fp2 &L0,
   fp2_quad_bcast<3>(T.z, s);  // Z3 = v^3 Z1
   fp2_neg(T.x, X3);           // X3 = v A
   fp2_neg(U, U);              // u (R - A)
+  fp2_sub(T.y, U, R2);
+}
+
+// Miller doubling step across a row (gang_line_dbl's levels): X Y, Y^2, Z^2, X^2 |
+// A (B - F), G^2, E^2, Y Z | B H
+__device__ __forceinline__ void row_line_dbl(g2h &T, fp2 &L0, fp2 &L2, fp2 &L3, int l) {
+  fp2 A, B, C, X2;
+  row_mul4(A, B, C, X2, T.x, T.y, T.z, T.x, T.y, T.y, T.z, T.x, l);
+  fp2_half(A, A);     // XY/2
+  fp2 E, F, G, t1;
+  fp2_mul_3b(E, C);   // 3b'Z^2
+  fp2_add(F, E, E);
+  fp2_add(F, F, E);   // 3E
+  fp2_sub(L0, E, B);
+  fp2_mul3(L2, X2);
+  fp2_sub(t1, B, F);
+  fp2_add(G, B, F);
+  fp2_half(G, G);
+  fp2 X3, G2, E2, H;
+  row_mul4(X3, G2, E2, H, A, G, E, T.y, t1, G, E, T.z, l);
+  fp2_add(H, H, H);   // 2YZ
+  fp2_neg(L3, H);
+  T.x = X3;           // X3 = A (B - F)
+  fp2_mul3(E2, E2);
+  fp2_sub(T.y, G2, E2);  // Y3 = G^2 - 3E^2
+  fp2 w;
+  row_mul4(T.z, w, w, w, B, B, B, B, H, H, H, H, l);  // Z3 = B H
+}
+
+// Miller addition step across a row (gang_line_add_aff's four levels)
+__device__ __forceinline__ void row_line_add_aff(g2h &T, const g2a &Q, fp2 &L0, fp2 &L2, fp2 &L3,
+                                                 int l) {
+  fp2 yZ, xZ, th, la, w;
+  row_mul4(yZ, xZ, w, w, Q.y, Q.x, Q.y, Q.x, T.z, T.z, T.z, T.z, l);
+  fp2_sub(th, T.y, yZ);
+  fp2_sub(la, T.x, xZ);
+  fp2 P0, P1, uu, vv;
+  row_mul4(P0, P1, uu, vv, th, la, th, la, Q.x, Q.y, th, la, l);
+  fp2_sub(L0, P0, P1);  // theta x2 - lambda y2
+  fp2_neg(L2, th);
+  L3 = la;
+  fp2 vvv, R, A, t;
+  row_mul4(vvv, R, A, w, vv, vv, uu, uu, la, T.x, T.z, T.z, l);
+  fp2_neg(vvv, vvv);    // v^3 = -lambda^3
+  fp2_sub(A, A, vvv);
+  fp2_sub(A, A, R);
+  fp2_sub(A, A, R);
+  fp2_sub(t, R, A);
+  fp2 X3, U, R2;
+  row_mul4(X3, U, R2, T.z, la, th, vvv, vvv, A, t, T.y, T.z, l);  // Z3 = v^3 Z1
+  fp2_neg(T.x, X3);     // X3 = v A
+  fp2_neg(U, U);        // u (R - A)
   fp2_sub(T.y, U, R2);
 }
 

@@ -20,6 +20,9 @@ constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t kLaneRegimeSets = 32768;   // G1 products, MSM folds
 constexpr uint32_t kLaneRegimeClear = 32768;  // cofactor clearing
 constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
+// ... and Miller lines of up to this many pairs run on 16-lane DPP rows (bls_gang.h),
+// 16 x 4096 lanes being one wave per SIMD
+constexpr uint32_t kRowRegimeMax = 6144;
 // line-coefficient buffer bound: above it the Miller lines are made in event slices
 constexpr size_t kLineBudget = (size_t)1 << 30;
 

@@ -1,0 +1,10 @@
+# 16-lane row gangs for small launches (clear, lines): GPU suite + B=1 + default + B=4 + C1
+set -o pipefail
+O=gpurun_out/r2ab
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 &&
+timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu --batches 1 > $O/bench_b1.txt 2>&1 &&
+timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu > $O/bench_c2.txt 2>&1 &&
+timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu --batches 4 > $O/bench_b4.txt 2>&1 &&
+timeout -k 10 300 python3 bench.py --config C1 --steps 40 --warmup 5 > $O/bench_c1.txt 2>&1
