@@ -144,7 +144,7 @@ def main():
     ap.add_argument("--sets", type=int, default=0, help="override the per-config batch size")
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight per GPU: step k runs on stream k %% inflight (1 GPU only)")
-    ap.add_argument("--batches", type=int, default=12,
+    ap.add_argument("--batches", type=int, default=16,
                     help="C2: independent batches per step, verified as segments of ONE device submission "
                          "(each its own random linear combination, final exponentiation and verdict), as "
                          "the engine's coalescer merges concurrent callers")
@@ -415,7 +415,7 @@ def main():
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4),
                 "peak": round(peak / 1e12, 3), "unit": "Tmad64/s",
                 "frac": round(ach / (peak / 1e12), 5) if peak else None,
-                "traffic": pmc_traffic(dom, cfg == "C2" and args.sets in (0, 4096) and args.batches == 12
+                "traffic": pmc_traffic(dom, cfg == "C2" and args.sets in (0, 4096) and args.batches == 16
                                        and args.inflight == 1),
                 "avg_launch_ms": round(tot_ms / ncalls, 4),
                 "path": {"fpmul_per_step": leg.path_fpmul(),

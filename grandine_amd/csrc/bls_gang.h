@@ -294,7 +294,7 @@ __device__ __forceinline__ void gang1_add(g1j &r, const g1j &a, const g1j &b, in
 
 // ---------------------------------------------------------------- 16-lane row gangs
 // For small launches (a lone 4096-set batch fills 256 of 1024 SIMDs with quads): one DPP
-// row (16 lanes) per pair in the Miller-line kernel.  Each dependency level issues up to
+// row (16 lanes) per point.  Each dependency level issues up to
 // four Fp2 products at once, quad j of the row computing product j as three Karatsuba Fp
 // products (lanes k = 0, 1, 2; lane 3 repeats 2), so a level costs ONE Fp product of
 // latency: Miller doubling step 3 levels (quad: 7 products), addition step 4 (quad: 12).
@@ -344,6 +344,83 @@ __device__ __forceinline__ void row_mul4(fp2 &R0, fp2 &R1, fp2 &R2, fp2 &R3, con
   fp2_row_bcast<4>(R1, c);
   fp2_row_bcast<8>(R2, c);
   fp2_row_bcast<12>(R3, c);
+}
+
+// dbl-2009-l across a row (gang_dbl's three levels), r may alias p
+__device__ __forceinline__ void row_dbl(g2j &r, const g2j &p, int l) {
+  fp2 t, A, B, W, Z2;
+  f_add(t, p.y, p.z);
+  row_mul4(A, B, W, Z2, p.x, p.y, t, p.z, p.x, p.y, t, p.z, l);
+  fp2 E, C, U, F, x;
+  f_add(t, p.x, B);  // X + B
+  f_sub(W, W, B);
+  f_sub(r.z, W, Z2);  // Z3 = 2YZ
+  f_dbl(E, A);
+  f_add(E, E, A);     // E = 3A
+  row_mul4(C, U, F, x, B, t, E, E, B, t, E, E, l);
+  f_sub(U, U, A);
+  f_sub(U, U, C);
+  f_dbl(U, U);        // D
+  f_sub(F, F, U);
+  f_sub(r.x, F, U);   // X3 = F - 2D
+  f_sub(t, U, r.x);
+  row_mul4(t, x, x, x, E, E, E, E, t, t, t, t, l);  // E (D - X3)
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_sub(r.y, t, C);   // Y3 = E (D - X3) - 8C
+}
+
+// add-2007-bl across a row (gang_add's five levels), r = a + b, r may alias a
+__device__ __forceinline__ void row_add(g2j &r, const g2j &a, const g2j &b, int l) {
+  if (jac_is_inf(b)) {
+    r = a;
+    return;
+  }
+  if (jac_is_inf(a)) {
+    r = b;
+    return;
+  }
+  fp2 Z1Z1, Z2Z2, U1, U2, S1, S2;
+  row_mul4(Z1Z1, Z2Z2, S1, S2, a.z, b.z, a.y, b.y, a.z, b.z, b.z, a.z, l);
+  row_mul4(U1, U2, S1, S2, a.x, b.x, S1, S2, Z2Z2, Z1Z1, Z2Z2, Z1Z1, l);
+  fp2 H, R, t, w;
+  fp2_sub(H, U2, U1);
+  fp2_sub(R, S2, S1);
+  fp2_add(R, R, R);  // r = 2 (S2 - S1)
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(R)) {
+      row_dbl(r, b, l);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  fp2 H2, ZZ, I, R2, Zs;
+  fp2_add(H2, H, H);
+  fp2_add(ZZ, a.z, b.z);
+  row_mul4(I, R2, Zs, w, H2, R, ZZ, ZZ, H2, R, ZZ, ZZ, l);
+  fp2_sub(Zs, Zs, Z1Z1);
+  fp2_sub(Zs, Zs, Z2Z2);  // 2 Z1 Z2
+  fp2 J, V;
+  row_mul4(J, V, r.z, w, H, U1, Zs, Zs, I, I, H, H, l);  // Z3 = 2 Z1 Z2 H
+  fp2_sub(t, R2, J);
+  fp2_sub(t, t, V);
+  fp2_sub(r.x, t, V);  // X3 = r^2 - J - 2V
+  fp2_sub(t, V, r.x);
+  row_mul4(t, S1, w, w, R, S1, R, S1, t, J, t, J, l);
+  fp2_add(S1, S1, S1);
+  fp2_sub(r.y, t, S1);  // Y3 = r (V - X3) - 2 S1 J
+}
+
+// [|x|]P with row doublings and additions
+__device__ __forceinline__ void row_mul_by_xabs(g2j &r, const g2j &p, int l) {
+  g2j acc = p;
+  for (int i = 62; i >= 0; i--) {
+    row_dbl(acc, acc, l);
+    if ((k::X_ABS >> i) & 1) row_add(acc, acc, p, l);
+  }
+  r = acc;
 }
 
 // [|x|]P with quad-cooperative doublings and additions

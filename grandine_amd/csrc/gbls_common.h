@@ -23,6 +23,7 @@ constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
 // ... and Miller lines of up to this many pairs run on 16-lane DPP rows (bls_gang.h),
 // 16 x 4096 lanes being one wave per SIMD
 constexpr uint32_t kRowRegimeMax = 6144;
+constexpr uint32_t kRowClearMax = 1024;  // cofactor clearing on rows (tiny launches only)
 // line-coefficient buffer bound: above it the Miller lines are made in event slices
 constexpr size_t kLineBudget = (size_t)1 << 30;
 

@@ -46,6 +46,39 @@ __global__ void __launch_bounds__(WG) k_h2c_clear(const g2j *Q, uint32_t n, g2a 
   if (q == 0) H[i] = o;
 }
 
+// Same sequence on a 16-lane row (tiny launches: the latency regime)
+__device__ __forceinline__ void row_clear_cofactor_g2(g2j &r, const g2j &p, int l) {
+  g2j t1, t2, t3;
+  row_mul_by_xabs(t1, p, l);
+  jac_neg(t1, t1);        // t1 = [x]P
+  g2_psi(t2, p);
+  row_add(t2, t2, t1, l);     // t1 + psi(P)
+  row_mul_by_xabs(t3, t2, l);
+  jac_neg(t3, t3);        // t3 = [x](t1 + psi(P))
+  jac_neg(t1, t1);
+  row_add(t3, t3, t1, l);     // - t1
+  row_dbl(t1, p, l);
+  g2_psi2(t1, t1);
+  row_add(t3, t3, t1, l);     // + psi^2(2P)
+  g2_psi(t1, p);
+  jac_neg(t1, t1);
+  row_add(t3, t3, t1, l);     // - psi(P)
+  jac_neg(t1, p);
+  row_add(r, t3, t1, l);      // - P
+}
+__global__ void __launch_bounds__(WG) k_h2c_clear_row(const g2j *Q, uint32_t n, g2a *H) {
+  uint32_t t = blockIdx.x * WG + threadIdx.x;
+  uint32_t i = t >> 4;
+  int l = (int)(t & 15);
+  if (i >= n) return;  // whole rows
+  g2j a = Q[2 * i], b = Q[2 * i + 1], h;
+  row_add(a, a, b, l);
+  row_clear_cofactor_g2(h, a, l);
+  g2a o;
+  jac_to_aff(o, h);
+  if (l == 0) H[i] = o;
+}
+
 // one lane per message (serial clear_cofactor_g2): for launches that fill the chip
 __global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n, g2a *H) {
   uint32_t i = blockIdx.x * WG + threadIdx.x;
@@ -62,6 +95,8 @@ void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   if (!n) return;
   if (n >= kLaneRegimeClear)
     k_h2c_clear_lane<<<nblk(n), WG, 0, st>>>(Q, n, H);
+  else if (n <= kRowClearMax)
+    k_h2c_clear_row<<<nblk((size_t)n * 16), WG, 0, st>>>(Q, n, H);
   else
     k_h2c_clear<<<nblk((size_t)n * 4), WG, 0, st>>>(Q, n, H);
 }
