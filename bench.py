@@ -6,11 +6,13 @@ Default workload (BASELINE.json configs[1], SURVEY.md 8(d) "C2"): synthetic batc
 sig_i = sk_i * H(m_i), nonzero 64-bit random scalars r_i -- each verified by ONE
 random-linear-combination batch check, exactly Signature::multi_verify (reference
 bls/src/signature.rs:95-129, reached from MultiVerifier::finish,
-helper_functions/src/verifier.rs:301-323).  A "step" = --batches (default 4) such
-batches in flight on one GPU, submitted together as segments of one device call the way
-the engine's cross-caller coalescer merges concurrent MultiVerifier::finish calls: every
-batch keeps its own scalars, its own S = sum r_i sig_i, its own final exponentiation and
-its own verdict.  Inputs are resident in HBM (decompressed points, as blst takes them);
+helper_functions/src/verifier.rs:301-323).  A "step" = --batches (default 16) such
+batches, submitted together as segments of one device call the way the engine's
+cross-caller coalescer merges concurrent MultiVerifier::finish calls: every batch keeps
+its own scalars, its own S = sum r_i sig_i, its own final exponentiation and its own
+verdict.  --inflight (default 2) submissions run at once on separate streams (step k on
+stream k mod 2), as the coalescer keeps two leaders per device: one step's serial tail
+(Horner, final exponentiation) overlaps the next step's hash_to_G2.  Inputs are resident in HBM (decompressed points, as blst takes them);
 hash_to_G2 of every message, both scalar sides, the Miller products and the final
 exponentiations all run inside the timed region.  The same run also times ONE batch per
 step ("single_batch": the 4096-set latency view).
@@ -142,8 +144,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "C5"])
     ap.add_argument("--sets", type=int, default=0, help="override the per-config batch size")
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="batches in flight per GPU: step k runs on stream k %% inflight (1 GPU only)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="submissions in flight per GPU: step k runs on stream k %% inflight, so one step's "
+                         "serial tail (Horner, final exponentiation) overlaps the next step's hash_to_G2, as "
+                         "the engine's coalescer keeps two leaders per device")
     ap.add_argument("--batches", type=int, default=16,
                     help="C2: independent batches per step, verified as segments of ONE device submission "
                          "(each its own random linear combination, final exponentiation and verdict), as "
@@ -237,12 +241,13 @@ def main():
         d_rands = torch.tensor(to_i64(rands), dtype=torch.int64, device=dev)
         d_idx = dnp(idx) if idx is not None else None
         d_off = dnp(off) if off is not None else None
-        d_verdicts = [torch.full((nb,), -1, dtype=torch.int32, device=dev) for _ in range(max(1, args.inflight))]
-        d_verdict = d_verdicts[0]
-        d_part = torch.zeros(nb * 576, dtype=torch.uint8, device=dev)
-        d_err = torch.zeros(nb, dtype=torch.int32, device=dev)
-        d_parts = torch.zeros(world * nb * 576, dtype=torch.uint8, device=dev)
-        d_errs = torch.zeros(world * nb, dtype=torch.int32, device=dev)
+        # per in-flight slot: verdicts, and for N > 1 the partial / error buffers of the exchange
+        slots = max(1, args.inflight)
+        d_verdicts = [torch.full((nb,), -1, dtype=torch.int32, device=dev) for _ in range(slots)]
+        d_part = [torch.zeros(nb * 576, dtype=torch.uint8, device=dev) for _ in range(slots)]
+        d_err = [torch.zeros(nb, dtype=torch.int32, device=dev) for _ in range(slots)]
+        d_parts = [torch.zeros(world * nb * 576, dtype=torch.uint8, device=dev) for _ in range(slots)]
+        d_errs = [torch.zeros(world * nb, dtype=torch.int32, device=dev) for _ in range(slots)]
         seg = G.u32_array([n * b // nb for b in range(nb + 1)])
         leg.units = n
         leg.segments = nb
@@ -251,8 +256,8 @@ def main():
             st = cur_stream()
             pidx = ptr(d_idx) if d_idx is not None else None
             poff = ptr(d_off) if d_off is not None else None
+            v = d_verdicts[slot]
             if world == 1:
-                v = d_verdicts[slot]
                 if cfg == "C2":
                     rc = L.gbls_multi_verify_segments_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n,
                                                              seg, nb, ptr(v), st)
@@ -263,19 +268,19 @@ def main():
                 return
             if cfg == "C2":
                 rc = L.gbls_multi_verify_partials_device(ptr(d_msgs), ptr(d_sigs), ptr(d_pks), ptr(d_rands), n, seg,
-                                                         nb, ptr(d_part), ptr(d_err), st)
+                                                         nb, ptr(d_part[slot]), ptr(d_err[slot]), st)
             else:
                 rc = L.gbls_multi_verify_indexed_partials_device(ptr(d_msgs), ptr(d_sigs), pidx, poff, ptr(d_rands),
-                                                                 n, seg, 1, ptr(d_part), ptr(d_err), st)
+                                                                 n, seg, 1, ptr(d_part[slot]), ptr(d_err[slot]), st)
             G.check(rc, "multi_verify partials")
-            dist.all_gather_into_tensor(d_parts, d_part)
-            dist.all_gather_into_tensor(d_errs, d_err)
-            rc = L.gbls_final_verify_partials_device(ptr(d_parts), ptr(d_errs), world, nb, ptr(d_verdict),
+            dist.all_gather_into_tensor(d_parts[slot], d_part[slot])
+            dist.all_gather_into_tensor(d_errs[slot], d_err[slot])
+            rc = L.gbls_final_verify_partials_device(ptr(d_parts[slot]), ptr(d_errs[slot]), world, nb, ptr(v),
                                                      cur_stream())
             G.check(rc, "final_verify_partials")
 
         def verdict_ok():
-            return all(bool((v == G.SUCCESS).all()) for v in (d_verdicts if world == 1 else [d_verdict]))
+            return all(bool((v == G.SUCCESS).all()) for v in d_verdicts)
 
         leg.stage_units = lambda s: {"k_ml_group": n + nb, "k_ml_reduce": n + nb, "k_lines_S": nb,
                                      "k_ml_horner": nb, "k_final_verdict": nb,
@@ -328,7 +333,7 @@ def main():
     else:
         return bench_c1(args, L, G, F, np)
 
-    D = max(1, args.inflight) if world == 1 and cfg != "C3" else 1
+    D = max(1, args.inflight) if cfg != "C3" else 1
     streams = [torch.cuda.Stream() for _ in range(D)] if D > 1 else None
 
     def run(k):
@@ -416,7 +421,7 @@ def main():
                 "peak": round(peak / 1e12, 3), "unit": "Tmad64/s",
                 "frac": round(ach / (peak / 1e12), 5) if peak else None,
                 "traffic": pmc_traffic(dom, cfg == "C2" and args.sets in (0, 4096) and args.batches == 16
-                                       and args.inflight == 1),
+                                       and args.inflight == 2),
                 "avg_launch_ms": round(tot_ms / ncalls, 4),
                 "path": {"fpmul_per_step": leg.path_fpmul(),
                          "achieved": round(leg.path_fpmul() * MAD_PER_FPMUL * args.steps / dt / 1e12, 4),

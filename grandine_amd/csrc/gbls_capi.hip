@@ -229,8 +229,12 @@ struct Ctx {
   }
 };
 
+// k_ml_group launches of more than this many waves per SIMD pick G to fill whole rounds
+constexpr uint32_t kMlRounds = 2;
+
 struct Device {
   int hipdev = -1;
+  uint32_t nsimd = 1024;  // 4 SIMDs per CU
   std::mutex mu;
   std::condition_variable cv;
   std::vector<Ctx *> idle;
@@ -247,6 +251,9 @@ struct Engine {
   size_t reg_n = 0;
   std::atomic<bool> coalesce{true};
   size_t msm_min = kMsmMinPerSeg;  // segments at least this large use the bucket MSM
+  size_t line_budget = kLineBudget; // line-coefficient buffer bound per submission (bytes)
+  uint32_t ml_g = 0;                // forced k_ml_group group size (0: chosen per launch)
+  uint32_t ml_rounds = kMlRounds;   // k_ml_group waves per SIMD for large launches
 } g;
 
 // RAII lease of a context of one device: the idle context last used on the caller's
@@ -325,6 +332,10 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
   if (ids.empty()) return fail(GBLS_ERR_NO_DEVICE);
   g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
   if (const char *e = std::getenv("GBLS_MSM_MIN")) g.msm_min = std::strtoull(e, nullptr, 10);
+  if (const char *e = std::getenv("GBLS_LINE_BUDGET_MB"))
+    g.line_budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
+  if (const char *e = std::getenv("GBLS_ML_G")) g.ml_g = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char *e = std::getenv("GBLS_ML_ROUNDS")) g.ml_rounds = (uint32_t)std::strtoul(e, nullptr, 10);
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
   for (int id : ids) {
@@ -334,6 +345,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     for (int r = 0; r < replicas; r++) {
       g.devs.emplace_back(new Device());
       g.devs.back()->hipdev = id;
+      g.devs.back()->nsimd = 4u * (uint32_t)prop.multiProcessorCount;
     }
   }
   g.ready.store(true);
@@ -442,14 +454,35 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   // lines (sets on the main stream, extra pairs on side 2), later ones after it.
   const size_t event_bytes = (size_t)np * 72 * 4;
   int EC = ML_EVENTS;
-  if (event_bytes * ML_EVENTS > kLineBudget)
-    EC = (int)std::max<size_t>(1, kLineBudget / event_bytes);
+  if (event_bytes * ML_EVENTS > g.line_budget)
+    EC = (int)std::max<size_t>(1, g.line_budget / event_bytes);
   const bool sliced = EC < ML_EVENTS;
   const size_t line_words = (size_t)np * EC * 72;
-  // G: the largest power of two <= 64 that still gives >= 65536 lanes (one wave per
-  // SIMD) per group launch (EC events).
+  // G, the pairs per k_ml_group lane.  Small launches: the largest power of two <= 64 that
+  // still gives >= 65536 lanes per launch (EC events).  Large launches: the smallest G
+  // whose launch is at most ml_rounds waves per SIMD, EC x ceil(groups / 64) waves, so that
+  // the waves fill whole rounds of the chip's SIMDs (a launch just past a multiple of them
+  // idles most of the chip for one more wave-duration, at one wave per SIMD).
   uint32_t G = 1;
   while (G < 64 && (uint64_t)EC * np / (2 * G) >= 65536) G *= 2;
+  {
+    auto waves = [&](uint32_t gs) {
+      uint64_t ng = 0;
+      for (size_t s = 0; s < nseg; s++) ng += (seg_off[s + 1] - seg_off[s] + X + gs - 1) / gs;
+      return (uint64_t)EC * ((ng + WG - 1) / WG);
+    };
+    const uint64_t cap = (uint64_t)g.ml_rounds * d.nsimd;
+    uint32_t lo = 1, hi = (uint32_t)np;  // smallest G with waves(G) <= cap
+    while (lo < hi) {
+      uint32_t mid = lo + (hi - lo) / 2;
+      if (waves(mid) <= cap)
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
+    if (lo >= 8) G = lo;
+  }
+  if (g.ml_g) G = g.ml_g;
   std::vector<uint32_t> &tab = c.host_tab;
   tab.clear();
   tab.resize(np);

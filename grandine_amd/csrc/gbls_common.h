@@ -24,8 +24,10 @@ constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
 // 16 x 4096 lanes being one wave per SIMD
 constexpr uint32_t kRowRegimeMax = 6144;
 constexpr uint32_t kRowClearMax = 1024;  // cofactor clearing on rows (tiny launches only)
-// line-coefficient buffer bound: above it the Miller lines are made in event slices
-constexpr size_t kLineBudget = (size_t)1 << 30;
+// line-coefficient buffer bound per submission (19.6 KB per pair: 4 GB = 214k pairs,
+// a C5 shard of 131 072 sets unsliced; tiny next to 288 GB of HBM): above it the Miller
+// lines are made in event slices (GBLS_LINE_BUDGET_MB overrides it)
+constexpr size_t kLineBudget = (size_t)4 << 30;
 
 inline unsigned nblk(size_t n, unsigned per = WG) { return (unsigned)((n + per - 1) / per); }
 

@@ -283,6 +283,20 @@ def test_bucket_msm_parity_subprocess():
     assert res["zero_scalar"] == 5
 
 
+def test_sliced_lines_subprocess():
+    """Event-sliced Miller lines (GBLS_LINE_BUDGET_MB=16: a 4096-set batch in slices of
+    a few events, the running points in HBM between slices): single-batch verdicts equal
+    the C oracle's, and a 4-segment batch flags exactly the segment with swapped
+    signatures."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_sliced.py")], capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["ref"] == [1, 0], res
+    assert res["single"] == [0, 5], res
+    assert [s[1:] for s in res["segments"]] == [[0, 0, 0, 0], [0, 0, 5, 0]], res
+
+
 # ------------------------------------------------------------------ registry (C4 / C5 shapes)
 N_REG = 1_700_000
 
