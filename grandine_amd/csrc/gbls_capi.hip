@@ -138,7 +138,7 @@ struct Ctx {
   size_t stage_cap = 0, stage_used = 0;
   std::vector<uint32_t> host_tab;  // table assembly, reused across calls
 
-  bool init(int dev) {
+  bool init(int dev, bool side2_high) {
     hipdev = dev;
     HIPCHK(hipSetDevice(dev));
     // the hash_to_G2 -> lines chain is the critical path: its stream gets the highest
@@ -147,7 +147,7 @@ struct Ctx {
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIPCHK(hipStreamCreateWithPriority(&own, hipStreamNonBlocking, greatest));
     HIPCHK(hipStreamCreateWithPriority(&side1, hipStreamNonBlocking, least));
-    HIPCHK(hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, least));
+    HIPCHK(hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, side2_high ? greatest : least));
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side1, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side2, hipEventDisableTiming));
@@ -254,6 +254,7 @@ struct Engine {
   size_t line_budget = kLineBudget; // line-coefficient buffer bound per submission (bytes)
   uint32_t ml_g = 0;                // forced k_ml_group group size (0: chosen per launch)
   uint32_t ml_rounds = kMlRounds;   // k_ml_group waves per SIMD for large launches
+  bool side2_high = false;          // signature-side stream (MSM) at the main stream's priority
 } g;
 
 // RAII lease of a context of one device: the idle context last used on the caller's
@@ -288,7 +289,7 @@ class Lease {
       d.cv.wait(lk);  // every context is leased: wait for one to come back
     }
     lk.unlock();
-    ok_ = fresh_ ? c_->init(d.hipdev) : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
+    ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high) : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
   }
   explicit Lease(Device &d) : Lease(d, false, nullptr) {}
   ~Lease() {
@@ -336,6 +337,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     g.line_budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
   if (const char *e = std::getenv("GBLS_ML_G")) g.ml_g = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char *e = std::getenv("GBLS_ML_ROUNDS")) g.ml_rounds = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char *e = std::getenv("GBLS_SIDE2_HIGH")) g.side2_high = std::atoi(e) != 0;
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
   for (int id : ids) {
