@@ -79,8 +79,6 @@ struct MsmPlan {
   int c, W;             // window bits, windows
   uint32_t nb;          // buckets (nseg * W * 2^(c-1))
   uint32_t max_chunks;  // bound on the chunk count (grid of the chunk kernel)
-  int folds;            // pairwise passes over a bucket's chunk sums
-  bool quad;            // quad-gang point operations (small launches)
   bool tree;            // per-window bucket trees (c = 13) or per-bucket pairs (c = 5)
   uint32_t extra;       // extra Miller pairs per segment: W (tree) or W * 2^(c-1)
   size_t o_cnt, o_start, o_cur, o_cstart, o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;

@@ -11,9 +11,9 @@
 //   1 k_msm_count    lane per set: bucket histogram (atomics), segment error flags
 //   2 k_msm_scan     one workgroup: bucket starts, chunk starts (K entries per chunk)
 //   3 k_msm_scatter  lane per set: (set | sign) into its buckets' lists
-//   4 k_msm_chunk    lane per chunk: sum of <= K affine points (mixed additions)
-//   5 k_msm_fold     per-bucket pairwise reduction of the chunk sums (log passes; DPP
-//                    quads when the launch is small, one lane per addition otherwise)
+//   4 k_msm_chunk    lane per chunk: sum of <= K affine points (mixed additions), then a
+//                    segmented fold of the wave's chunks by bucket through LDS (one
+//                    partial per bucket and wave; the bucket's reader adds them up)
 // The bucket sums X_{w,b} never go through a Horner chain of 60 doublings.  The weights
 // move to the G1 side of the pairing instead, where they are constants:
 //   e(-g1, S) = prod_{w,b} e(-[(b+1) 2^(c w)] g1, X_{w,b}),
@@ -21,15 +21,15 @@
 // point (bls_constants.h MSM_W5, tools/gen_constants.py).  With c = 5 that is
 // 13 * 16 = 208 pairs per segment (+5% Miller work at 4096 sets), and the G2 side has
 // no serial tail:
-//   6 k_msm_pairs    lane per bucket: affine X_{w,b}, its pair
+//   5 k_msm_pairs    lane per bucket: X_{w,b} (the bucket's partials), affine, its pair
 // With c = 13 (segments >= 2^16 sets, 4096 buckets per window) a per-window tree
 // first folds the weights (b + 1) into S_w, and the 5 window sums pair with
 // -[2^(13 w)] g1 (MSM_W13):
-//   6 k_msm_bucket   level-0 tree nodes
-//   7 k_msm_tree     per (segment, window), a binary tree over the buckets computing
+//   5 k_msm_bucket   level-0 tree nodes (the buckets' partials added up)
+//   6 k_msm_tree     per (segment, window), a binary tree over the buckets computing
 //                    S_w = sum_b (b+1) X_b with nodes (T = sum X, A = sum (b - lo) X):
 //                    T = T_L + T_R, A = A_L + A_R + 2^l T_R   (l = level)
-//   8 k_msm_wpairs   lane per window: affine S_w = A + T, its pair
+//   7 k_msm_wpairs   lane per window: affine S_w = A + T, its pair
 // Infinite signatures and zero scalars contribute nothing (blst skips infinite
 // signatures; a zero scalar fails the batch through k_msm_count's flags).  An empty bucket is
 // the point at infinity, whose Miller pair is the identity.  Bucket order is
@@ -151,73 +151,72 @@ __global__ void __launch_bounds__(WGR) k_msm_scatter(const g2a *sigs, const uint
   }
 }
 
-// point additions of the fold passes: on a DPP quad (Q, latency regime) or one lane
-template <bool Q>
-__device__ __forceinline__ void p_add(g2j &r, const g2j &a, const g2j &b, int q) {
-  if (Q) {
-    gang_add(r, a, b, q);
-  } else {
-    g2j t = b;
-    jac_add(r, a, t);
-  }
-}
-template <bool Q>
-__device__ __forceinline__ uint32_t p_unit(int &q) {
-  uint32_t t = blockIdx.x * WG + threadIdx.x;
-  q = Q ? (int)(t & 3) : 0;
-  return Q ? t >> 2 : t;
-}
-
-// chunk j: sum of <= K affine points of one bucket (found by binary search over cstart)
+// chunk j: sum of <= K affine points of one bucket (found by binary search over cstart),
+// then, within the wave, a segmented pairwise fold of the wave's chunks by bucket: every
+// bucket's chunks inside one wave end up summed in its first chunk there (levels only
+// while some run of same-bucket chunks in the wave is longer than the step).  A bucket
+// thus leaves one partial per wave it touches, at its first chunk cstart[b] and at each
+// wave boundary 64 w inside [cstart[b], cstart[b + 1]) (msm_bucket_sum).
 __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_t *list,
                                                   const uint32_t *start, const uint32_t *cstart,
                                                   uint32_t nb, uint32_t max_chunks, g2j *chunk) {
-  uint32_t j = blockIdx.x * WG + threadIdx.x;
-  if (j >= max_chunks || j >= cstart[nb]) return;
-  uint32_t lo = 0, hi = nb;  // largest b with cstart[b] <= j
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (cstart[mid] <= j)
-      lo = mid;
-    else
-      hi = mid;
-  }
-  uint32_t b = lo;
-  uint32_t e0 = start[b] + (j - cstart[b]) * MSM_K;
-  uint32_t e1 = min(e0 + MSM_K, start[b + 1]);
+  __shared__ g2j xs[WG];
+  const uint32_t lane = threadIdx.x, base = blockIdx.x * WG;
+  const uint32_t j = base + lane, total = cstart[nb];
+  const bool live = j < max_chunks && j < total;
   g2j acc;
   jac_set_inf(acc);
-  for (uint32_t e = e0; e < e1; e++) {
-    uint32_t v = list[e];
-    g2a p = sigs[v & 0x7fffffffu];
-    if (v >> 31) fp2_neg(p.y, p.y);
-    jac_add_aff(acc, acc, p);
+  uint32_t lo = 0;
+  if (live) {
+    uint32_t hi = nb;  // largest b with cstart[b] <= j
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (cstart[mid] <= j)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    uint32_t e0 = start[lo] + (j - cstart[lo]) * MSM_K;
+    uint32_t e1 = min(e0 + MSM_K, start[lo + 1]);
+    for (uint32_t e = e0; e < e1; e++) {
+      uint32_t v = list[e];
+      g2a p = sigs[v & 0x7fffffffu];
+      if (v >> 31) fp2_neg(p.y, p.y);
+      jac_add_aff(acc, acc, p);
+    }
   }
-  chunk[j] = acc;
+  // this lane's position in its bucket's run inside the wave, and the run's end (lanes)
+  const uint32_t first = live ? (cstart[lo] > base ? cstart[lo] - base : 0u) : lane;
+  const uint32_t end = live ? min((uint32_t)WG, cstart[lo + 1] - base) : lane + 1;
+  const uint32_t k = lane - first;
+  uint32_t run = end - first;  // wave maximum of the run lengths
+  for (int o = 32; o >= 1; o >>= 1) run = max(run, (uint32_t)__shfl_xor((int)run, o));
+  for (uint32_t st = 1; st < run; st <<= 1) {
+    xs[lane] = acc;
+    __syncthreads();
+    if ((k & (2 * st - 1)) == 0 && lane + st < end) {
+      g2j x = xs[lane + st];
+      jac_add(acc, acc, x);
+    }
+    __syncthreads();
+  }
+  if (live && k == 0) chunk[j] = acc;
 }
 
-// pass p of the per-bucket pairwise reduction of chunk sums: chunk k of bucket b (k a
-// multiple of 2^(p+1)) absorbs chunk k + 2^p; log2(max chunks per bucket) passes leave
-// every bucket's sum in its first chunk (depth log, whatever the digit distribution)
-template <bool Q>
-__global__ void __launch_bounds__(WG) k_msm_fold(const uint32_t *cstart, uint32_t nb,
-                                                 uint32_t max_chunks, int p, g2j *chunk) {
-  int q;
-  uint32_t j = p_unit<Q>(q);
-  if (j >= max_chunks || j >= cstart[nb]) return;
-  uint32_t lo = 0, hi = nb;
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (cstart[mid] <= j)
-      lo = mid;
-    else
-      hi = mid;
+// sum of bucket b: its first chunk's partial plus the partials at the chunk waves' starts
+// inside the bucket's chunk range (k_msm_chunk)
+__device__ __forceinline__ void msm_bucket_sum(g2j &x, const g2j *chunk, const uint32_t *cstart,
+                                               uint32_t b) {
+  const uint32_t c0 = cstart[b], c1 = cstart[b + 1];
+  if (c1 == c0) {
+    jac_set_inf(x);
+    return;
   }
-  uint32_t k = j - cstart[lo], step = 1u << p;
-  if ((k & (2 * step - 1)) != 0 || j + step >= cstart[lo + 1]) return;
-  g2j a = chunk[j], x = chunk[j + step];
-  p_add<Q>(a, a, x, q);
-  if (q == 0) chunk[j] = a;
+  x = chunk[c0];
+  for (uint32_t w = (c0 / WG + 1) * WG; w < c1; w += WG) {
+    g2j y = chunk[w];
+    jac_add(x, x, y);
+  }
 }
 
 // the constant G1 half of an extra pair: table entry k (x, y Montgomery), c = 1
@@ -240,10 +239,7 @@ __global__ void __launch_bounds__(WG) k_msm_pairs(const g2j *chunk, const uint32
   if (t >= nb) return;
   uint32_t s = t / per_seg, k = t % per_seg;
   g2j x;
-  if (cstart[t + 1] > cstart[t])
-    x = chunk[cstart[t]];
-  else
-    jac_set_inf(x);
+  msm_bucket_sum(x, chunk, cstart, t);
   g2a a;
   jac_to_aff(a, x);
   g1s w;
@@ -258,9 +254,10 @@ __global__ void __launch_bounds__(WG) k_msm_bucket(const g2j *chunk, const uint3
                                                    uint32_t nb, g2j *T, g2j *A) {
   uint32_t b = blockIdx.x * WG + threadIdx.x;
   if (b >= nb) return;
-  g2j inf;
+  g2j x, inf;
+  msm_bucket_sum(x, chunk, cstart, b);
   jac_set_inf(inf);
-  T[b] = cstart[b + 1] > cstart[b] ? chunk[cstart[b]] : inf;
+  T[b] = x;
   A[b] = inf;
 }
 
@@ -307,9 +304,7 @@ __global__ void __launch_bounds__(WG) k_msm_wpairs(const g2j *T, const g2j *A, u
 // Window widths dividing 65 (64-bit scalars + the signed-digit carry), so that no window
 // is nearly empty (a 2-bit top window would pile every set into two buckets): c = 5
 // (13 windows, 16 buckets each, one Miller pair per bucket) for segments up to 2^16 sets,
-// else c = 13 (5 windows of 4096 buckets, per-window trees, one pair per window).  The
-// folds run on quad gangs below kLaneRegimeSets sets in the launch, one lane per
-// addition above.
+// else c = 13 (5 windows of 4096 buckets, per-window trees, one pair per window).
 MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   uint32_t avg = nseg ? n / nseg : n;
   MsmPlan p;
@@ -318,11 +313,8 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.W = 65 / p.c;
   p.tree = p.c == 13;
   p.extra = p.tree ? (uint32_t)p.W : ((uint32_t)p.W << (p.c - 1));
-  p.quad = n < kLaneRegimeSets;
   p.nb = nseg * ((uint32_t)p.W << (p.c - 1));
   p.max_chunks = (uint32_t)(((uint64_t)p.W * n + MSM_K - 1) / MSM_K) + p.nb;
-  p.folds = 0;
-  while ((1u << p.folds) < (uint32_t)((avg + MSM_K - 1) / MSM_K)) p.folds++;
   size_t o = 0;
   auto take = [&](size_t bytes) {
     size_t at = o;
@@ -363,13 +355,6 @@ void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
                                               list);
   k_msm_chunk<<<nblk(p.max_chunks), WG, 0, st>>>(sigs, list, start, cstart, p.nb, p.max_chunks,
                                                  chunk);
-  for (int f = 0; f < p.folds + 1; f++) {  // + 1: the digit distribution is not exactly flat
-    if (p.quad)
-      k_msm_fold<true><<<nblk(4 * (size_t)p.max_chunks), WG, 0, st>>>(cstart, p.nb, p.max_chunks,
-                                                                      f, chunk);
-    else
-      k_msm_fold<false><<<nblk(p.max_chunks), WG, 0, st>>>(cstart, p.nb, p.max_chunks, f, chunk);
-  }
   if (!p.tree) {
     k_msm_pairs<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, p.extra, n, seg_off,
                                            empty_is_error, P, H, seg_err);

@@ -7,7 +7,7 @@ T=${1:?tag}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu"
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 &&
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 > $O/bench_c2.txt 2>&1 &&
 timeout -k 10 300 python3 bench.py --config C1 --steps 40 --warmup 5 > $O/bench_c1.txt 2>&1 &&
