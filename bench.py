@@ -404,13 +404,14 @@ def main():
     ns = L.gbls_profile_read(ms, calls, nst)
     stages = {L.gbls_stage_name(i).decode(): (ms[i], calls[i]) for i in range(ns) if calls[i]}
     peak = L.gbls_measure_mad64_peak()
-    # dominant kernel: the longest single-kernel stage with algorithmic work of its own
-    # (rocprofv3 reports the same kernel's duration).  Not roofline rows: the multi-kernel
-    # stages k_msm / k_ml_reduce / k_g2sum, and k_lines_S, which mostly waits for SIMDs
-    # held by the main stream.
+    # dominant kernel: the single-kernel stage with the most algorithmic work per step
+    # (W x units; rocprofv3 reports the same kernel's duration).  Not by wall time: with two
+    # submissions in flight a low-priority side-stream stage (k_mv_g1mul) spans most of a
+    # step waiting for SIMDs.  Not roofline rows: the multi-kernel stages k_msm /
+    # k_ml_reduce / k_g2sum, and k_lines_S.
     multi = {"k_msm", "k_ml_reduce", "k_g2sum", "k_lines_S"}
     cand = [k for k in stages if W_FPMUL.get(k, 0) > 0 and k not in multi]
-    dom = max(cand, key=lambda k: stages[k][0]) if cand else None
+    dom = max(cand, key=lambda k: leg.stage_units(k) * W_FPMUL[k]) if cand else None
     roof = None
     if dom:
         tot_ms, ncalls = stages[dom]

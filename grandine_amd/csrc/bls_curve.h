@@ -261,6 +261,56 @@ HD void mul_u64(jac<F> &r, const aff<F> &base, uint64_t k) {
   r = acc;
 }
 
+HD void g1j_sel(g1j &r, bool c, const g1j &a, const g1j &b) {  // r = c ? b : a
+  fp_sel(r.x, c, a.x, b.x);
+  fp_sel(r.y, c, a.y, b.y);
+  fp_sel(r.z, c, a.z, b.z);
+}
+// [k]P for an affine G1 base and a 64-bit scalar: signed 3-bit digits d_i in [-3, 4]
+// (k = sum d_i 8^i, 22 digits) over the table {P, 2P, 3P, 4P}, 65 doublings + 22 Jacobian
+// additions whatever k is.  Every lane runs the same instructions (the table entry and
+// a zero digit are selects), so a wave of lanes with different scalars does not pay
+// for both sides of every bit, as mul_u64's double-and-add does (63 doublings + 63 mixed
+// additions per wave): 807 Fp products against 1134.
+HD void g1_mul_u64_w3(g1j &r, const g1a &base, uint64_t k) {
+  g1j t0, t1, t2, t3;
+  jac_from_aff(t0, base);
+  jac_dbl(t1, t0);
+  jac_add(t2, t1, t0);
+  jac_dbl(t3, t1);
+  // carry into each window (LSB first), so the MSB-first loop can form its digit
+  uint32_t cmask = 0, carry = 0;
+#pragma unroll
+  for (int i = 0; i < 22; i++) {
+    cmask |= carry << i;
+    carry = ((uint32_t)((k >> (3 * i)) & 7u) + carry) > 4;  // 3 i <= 63
+  }
+  g1j acc;
+  jac_set_inf(acc);
+  const uint32_t top = (uint32_t)(k >> 63) + (cmask >> 21);  // top digit in [0, 2]
+  g1j_sel(acc, top == 1, acc, t0);
+  g1j_sel(acc, top == 2, acc, t1);
+#pragma unroll 1
+  for (int i = 20; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    jac_dbl(acc, acc);
+    jac_dbl(acc, acc);
+    int v = (int)((k >> (3 * i)) & 7u) + (int)((cmask >> i) & 1u);
+    if (v > 4) v -= 8;
+    const uint32_t m = (uint32_t)(v < 0 ? -v : v);
+    g1j q = t0, s;
+    g1j_sel(q, m == 2, q, t1);
+    g1j_sel(q, m == 3, q, t2);
+    g1j_sel(q, m == 4, q, t3);
+    fp ny;
+    fp_neg(ny, q.y);
+    fp_sel(q.y, v < 0, q.y, ny);
+    jac_add(s, acc, q);
+    g1j_sel(acc, m != 0, acc, s);
+  }
+  r = acc;
+}
+
 // [|x|]P for a Jacobian point (|x| = 0xd201000000010000, 6 set bits) -- callers negate.
 template <class F>
 HD void mul_by_xabs(jac<F> &r, const jac<F> &p) {

@@ -78,6 +78,15 @@ int h_g1_aggregate(const uint8_t *pks96, uint32_t n, uint8_t *out96) {
   std::memcpy(out96, &r, 96);
   return n ? ST_SUCCESS : ST_AGGR_TYPE_MISMATCH;
 }
+// windowed G1 scalar product (k_mv_g1mul_lane) against double-and-add: 1 if equal
+int h_g1_mul_w3_check(const uint8_t *pk96, uint64_t k) {
+  g1a p;
+  std::memcpy(&p, pk96, 96);
+  g1j a, b;
+  g1_mul_u64_w3(a, p, k);
+  mul_u64(b, p, k);
+  return jac_eq(a, b);
+}
 void h_sk_to_pk(const uint8_t *sk32, uint8_t *out96) {
   uint32_t s[8];
   for (int i = 0; i < 8; i++) {

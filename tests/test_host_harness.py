@@ -87,6 +87,21 @@ def test_wave12_product_matches_tower_product(H):
         assert o1.raw == o2.raw
 
 
+def test_g1_windowed_scalar_product(H):
+    """g1_mul_u64_w3 (k_mv_g1mul_lane: signed 3-bit windows over {P, 2P, 3P, 4P}) equals
+    the double-and-add mul_u64 on edge scalars (0, small, every digit value, top bit,
+    all ones) and random ones, and maps the point at infinity to infinity."""
+    import random
+    rng = random.Random(5)
+    H.h_g1_mul_w3_check.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    pts = [g1_b(O.sk_to_pk(sk)) for sk in (1, 7, 0x1234567890ABCDEF)] + [bytes(96)]
+    ks = [0, 1, 2, 3, 4, 5, 6, 7, 8, 0o4444, 0o3333, 0o77777, 1 << 63, (1 << 63) - 1, (1 << 64) - 1,
+          0x9E3779B97F4A7C15, 0x4924924924924924] + [rng.getrandbits(64) for _ in range(40)]
+    for p in pts:
+        for k in ks:
+            assert H.h_g1_mul_w3_check(p, k) == 1, (p.hex()[:16], k)
+
+
 def test_g1_decode_fixtures(H):
     for c in gold("g1_decode")["cases"]:
         out = ctypes.create_string_buffer(96)
