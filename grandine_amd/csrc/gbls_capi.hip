@@ -138,16 +138,18 @@ struct Ctx {
   size_t stage_cap = 0, stage_used = 0;
   std::vector<uint32_t> host_tab;  // table assembly, reused across calls
 
-  bool init(int dev, bool side2_high) {
+  bool init(int dev, bool side2_high, int prio_mode) {
     hipdev = dev;
     HIPCHK(hipSetDevice(dev));
     // the hash_to_G2 -> lines chain is the critical path: its stream gets the highest
     // priority, the key-side and signature-side streams (slack of several ms) the lowest
     int least = 0, greatest = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIPCHK(hipStreamCreateWithPriority(&own, hipStreamNonBlocking, greatest));
-    HIPCHK(hipStreamCreateWithPriority(&side1, hipStreamNonBlocking, least));
-    HIPCHK(hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, side2_high ? greatest : least));
+    // prio_mode (GBLS_PRIO_MODE, experiments): 1 = every stream high, 2 = every stream low
+    const int pm = prio_mode, hi = pm == 2 ? least : greatest, lo = pm == 1 ? greatest : least;
+    HIPCHK(hipStreamCreateWithPriority(&own, hipStreamNonBlocking, hi));
+    HIPCHK(hipStreamCreateWithPriority(&side1, hipStreamNonBlocking, lo));
+    HIPCHK(hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, side2_high ? hi : lo));
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side1, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_side2, hipEventDisableTiming));
@@ -255,6 +257,7 @@ struct Engine {
   uint32_t ml_g = 0;                // forced k_ml_group group size (0: chosen per launch)
   uint32_t ml_rounds = kMlRounds;   // k_ml_group waves per SIMD for large launches
   bool side2_high = false;          // signature-side stream (MSM) at the main stream's priority
+  int prio_mode = 0;                // 0: main high, sides low; 1: all high; 2: all low
 } g;
 
 // RAII lease of a context of one device: the idle context last used on the caller's
@@ -289,7 +292,7 @@ class Lease {
       d.cv.wait(lk);  // every context is leased: wait for one to come back
     }
     lk.unlock();
-    ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high) : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
+    ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high, g.prio_mode) : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
   }
   explicit Lease(Device &d) : Lease(d, false, nullptr) {}
   ~Lease() {
@@ -338,6 +341,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
   if (const char *e = std::getenv("GBLS_ML_G")) g.ml_g = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char *e = std::getenv("GBLS_ML_ROUNDS")) g.ml_rounds = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char *e = std::getenv("GBLS_SIDE2_HIGH")) g.side2_high = std::atoi(e) != 0;
+  if (const char *e = std::getenv("GBLS_PRIO_MODE")) g.prio_mode = std::atoi(e);
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
   for (int id : ids) {
