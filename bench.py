@@ -164,9 +164,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GBLS_BENCH_ONE_DEVICE=1 (rehearsal of the N-rank flow on a one-GPU box): every rank on
+    # cuda:0, gloo instead of RCCL (RCCL refuses two ranks on one device)
+    one_dev = os.environ.get("GBLS_BENCH_ONE_DEVICE") == "1"
     if world > 1:
+        local = 0 if one_dev else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -187,6 +194,16 @@ def main():
 
     def cur_stream():
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def gather(out, inp):
+        # the rank partials' exchange: one all-gather over RCCL (gloo rehearsal: list form)
+        if not one_dev:
+            dist.all_gather_into_tensor(out, inp)
+            return
+        torch.cuda.current_stream().synchronize()
+        parts = [torch.empty_like(inp) for _ in range(world)]
+        dist.all_gather(parts, inp)
+        out.copy_(torch.cat(parts))
 
     leg = Leg()
     cfg = args.config
@@ -273,8 +290,8 @@ def main():
                 rc = L.gbls_multi_verify_indexed_partials_device(ptr(d_msgs), ptr(d_sigs), pidx, poff, ptr(d_rands),
                                                                  n, seg, 1, ptr(d_part[slot]), ptr(d_err[slot]), st)
             G.check(rc, "multi_verify partials")
-            dist.all_gather_into_tensor(d_parts[slot], d_part[slot])
-            dist.all_gather_into_tensor(d_errs[slot], d_err[slot])
+            gather(d_parts[slot], d_part[slot])
+            gather(d_errs[slot], d_err[slot])
             rc = L.gbls_final_verify_partials_device(ptr(d_parts[slot]), ptr(d_errs[slot]), world, nb, ptr(v),
                                                      cur_stream())
             G.check(rc, "final_verify_partials")
