@@ -182,7 +182,8 @@ HD void sp_to_fp12(fp12 &r, const sp034 &s) {
   r.c1.c1 = s.a3;  // w^3 = v w
   fp2_zero(r.c1.c2);
 }
-// (a0 + a2 w^2 + a3 w^3)(b0 + b2 w^2 + b3 w^3): 6 Fp2 products (Karatsuba pairs)
+// (a0 + a2 w^2 + a3 w^3)(b0 + b2 w^2 + b3 w^3): 6 Fp2 products (Karatsuba pairs; the
+// operand sums stay unreduced, fp2_mul takes operands < 2p)
 HD void sp_mul_sp(fp12 &r, const sp034 &a, const sp034 &b) {
   fp2 t0, t2, t3, sa, sb, u;
   fp2_mul(t0, a.a0, b.a0);
@@ -194,43 +195,44 @@ HD void sp_mul_sp(fp12 &r, const sp034 &a, const sp034 &b) {
   // w^1: 0
   fp2_zero(r.c1.c0);
   // w^2: (a0+a2)(b0+b2) - t0 - t2
-  fp2_add(sa, a.a0, a.a2);
-  fp2_add(sb, b.a0, b.a2);
+  fp2_add_lazy(sa, a.a0, a.a2);
+  fp2_add_lazy(sb, b.a0, b.a2);
   fp2_mul(u, sa, sb);
   fp2_sub(u, u, t0);
   fp2_sub(r.c0.c1, u, t2);
   // w^3: (a0+a3)(b0+b3) - t0 - t3
-  fp2_add(sa, a.a0, a.a3);
-  fp2_add(sb, b.a0, b.a3);
+  fp2_add_lazy(sa, a.a0, a.a3);
+  fp2_add_lazy(sb, b.a0, b.a3);
   fp2_mul(u, sa, sb);
   fp2_sub(u, u, t0);
   fp2_sub(r.c1.c1, u, t3);
   // w^4: t2
   r.c0.c2 = t2;
   // w^5: (a2+a3)(b2+b3) - t2 - t3
-  fp2_add(sa, a.a2, a.a3);
-  fp2_add(sb, b.a2, b.a3);
+  fp2_add_lazy(sa, a.a2, a.a3);
+  fp2_add_lazy(sb, b.a2, b.a3);
   fp2_mul(u, sa, sb);
   fp2_sub(u, u, t2);
   fp2_sub(r.c1.c2, u, t3);
 }
 
-// a * (b0 + b1 v): 5 Fp2 products
+// a * (b0 + b1 v): 5 Fp2 products (canonical operands; the Karatsuba operand sums stay
+// unreduced, fp2_mul takes operands < 2p)
 HD void fp6_mul_01(fp6 &r, const fp6 &a, const fp2 &b0, const fp2 &b1) {
   fp2 t0, t1, s0, s1, c0, c1, c2;
   fp2_mul(t0, a.c0, b0);
   fp2_mul(t1, a.c1, b1);
-  fp2_add(s0, a.c1, a.c2);
+  fp2_add_lazy(s0, a.c1, a.c2);
   fp2_mul(c0, s0, b1);
   fp2_sub(c0, c0, t1);
   fp2_mul_xi(c0, c0);
   fp2_add(c0, c0, t0);
-  fp2_add(s0, a.c0, a.c1);
-  fp2_add(s1, b0, b1);
+  fp2_add_lazy(s0, a.c0, a.c1);
+  fp2_add_lazy(s1, b0, b1);
   fp2_mul(c1, s0, s1);
   fp2_sub(c1, c1, t0);
   fp2_sub(c1, c1, t1);
-  fp2_add(s0, a.c0, a.c2);
+  fp2_add_lazy(s0, a.c0, a.c2);
   fp2_mul(c2, s0, b0);
   fp2_sub(c2, c2, t0);
   fp2_add(c2, c2, t1);
