@@ -475,8 +475,9 @@ def main():
 def bench_c1(args, L, G, F, np):
     """C1: a mainnet-shaped block's signature sets (1 proposer + 1 RANDAO + 128 aggregate
     attestations of ~512 registry keys + a 512-key sync aggregate = 131 sets) through the
-    host-pointer ABI exactly as MultiVerifier::finish would call it (G2 decompression of
-    the 131 signatures, then one indexed multi_verify): per-call latency, PCIe included.
+    host-pointer ABI as MultiVerifier::finish calls it (G2 decompression of the 131
+    signatures fused into one indexed multi_verify submission; the two-call form, decompress
+    then verify, is timed beside it): per-call latency, PCIe included.
     Also: 64-set gossip batches (p2p/src/attestation_verifier.rs:37), serial and from 16
     concurrent threads (the node's verifier tasks)."""
     import threading
@@ -494,22 +495,32 @@ def bench_c1(args, L, G, F, np):
     G.check(L.gbls_g2_compress(sigs, n, comp_sigs), "compress")
     rands = F.rands(n, 1)
 
-    def finish():
+    pidx, poff = idx.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p)
+
+    def finish():  # one submission: device decompression fused into the batch verify
+        st = G.i32_array(n)
+        return L.gbls_multi_verify_compressed(msgs, comp_sigs, None, pidx, poff,
+                                              (ctypes.c_uint64 * n)(*rands), n, st)
+
+    def finish_two_calls():  # decompress, then verify (two submissions)
         dec = ctypes.create_string_buffer(192 * n)
         st = G.i32_array(n)
         G.check(L.gbls_g2_decompress(comp_sigs, n, dec, st), "decompress")
         assert all(st[i] == 0 for i in range(n))
-        return L.gbls_multi_verify_indexed(msgs, dec, idx.ctypes.data_as(ctypes.c_void_p),
-                                           off.ctypes.data_as(ctypes.c_void_p),
-                                           (ctypes.c_uint64 * n)(*rands), n)
+        return L.gbls_multi_verify_indexed(msgs, dec, pidx, poff, (ctypes.c_uint64 * n)(*rands), n)
 
-    for _ in range(args.warmup):
-        assert finish() == G.SUCCESS
-    lat = []
-    for _ in range(args.steps):
-        t = time.perf_counter()
-        assert finish() == G.SUCCESS
-        lat.append(time.perf_counter() - t)
+    def timed(fn):
+        for _ in range(args.warmup):
+            assert fn() == G.SUCCESS
+        out = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            assert fn() == G.SUCCESS
+            out.append(time.perf_counter() - t)
+        return sorted(out)
+
+    lat = timed(finish)
+    lat2 = timed(finish_two_calls)
     # gossip: 64 single-key sets per call
     gm, gs, gp, gr = F.c2_batch(64, seed=64)
     r64 = (ctypes.c_uint64 * 64)(*gr)
@@ -534,16 +545,17 @@ def bench_c1(args, L, G, F, np):
         x.join()
     conc = time.perf_counter() - t
     assert not errs
-    lat.sort()
     glat.sort()
     line = {"metric": "MultiVerifier::finish latency, mainnet-shaped block (C1)", "value": round(lat[len(lat) // 2] * 1e3, 3),
             "unit": "ms (p50)", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(sum(lat) / len(lat) * 1e3, 3), "higher_is_better": False, "scaling": "n/a",
             "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
             "data": "synthetic (seeded registry, committees and messages)",
-            "config": {"workload": "C1: %d sets (%d keys aggregated from the registry), host pointers, PCIe included"
-                                   % (n, int(off[-1])), "config": "C1"},
+            "config": {"workload": "C1: %d sets (%d keys aggregated from the registry), 96-byte signatures "
+                                   "decompressed on the device inside the verify submission, host pointers, PCIe "
+                                   "included" % (n, int(off[-1])), "config": "C1"},
             "p99_ms": round(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3, 3),
+            "decompress_then_verify_p50_ms": round(lat2[len(lat2) // 2] * 1e3, 3),
             "gossip64": {"p50_ms": round(glat[len(glat) // 2] * 1e3, 3),
                          "p99_ms": round(glat[min(len(glat) - 1, int(len(glat) * 0.99))] * 1e3, 3),
                          "concurrent_16_threads_sets_per_s": round(nthr * per * 64 / conc, 1)},

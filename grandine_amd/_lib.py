@@ -49,6 +49,7 @@ EXPORTS = [
     "gbls_g1_aggregate_indexed",
     "gbls_fast_aggregate_verify_indexed",
     "gbls_multi_verify_indexed",
+    "gbls_multi_verify_compressed",
     "gbls_multi_verify_bisect",
     "gbls_multi_verify_indexed_segments_device",
     "gbls_fast_aggregate_verify_indexed_device",
@@ -127,6 +128,7 @@ def load_library():
                 "gbls_g1_aggregate_indexed": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
                 "gbls_fast_aggregate_verify_indexed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
                 "gbls_multi_verify_indexed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
+                "gbls_multi_verify_compressed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
                 "gbls_multi_verify_bisect": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
                 "gbls_fast_aggregate_verify_indexed_device": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp]),
                 "gbls_multi_verify_indexed_partials_device": (

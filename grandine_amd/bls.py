@@ -247,6 +247,28 @@ class Signature:
         return L.gbls_multi_verify(G.buf(b"".join(msgs)), G.buf(b"".join(s.raw for s in sigs)),
                                    G.buf(b"".join(p.raw for p in pks)), G.u64_array(randoms), n) == G.SUCCESS
 
+    @staticmethod
+    def multi_verify_compressed(messages: Iterable[bytes], signature_bytes: Iterable[bytes],
+                                public_keys: Iterable[PublicKey], randoms: Sequence[int] = None) -> int:
+        """MultiVerifier::finish's decompress + multi_verify (verifier.rs:301-323) as one device
+        submission (gbls_multi_verify_compressed): 0 = valid, 5 = VERIFY_FAIL, otherwise the
+        first signature's decompression status (finish's Err(DecompressionFailed))."""
+        msgs = [bytes(m) for m in messages]
+        sigs = [bytes(s) for s in signature_bytes]
+        pks = list(public_keys)
+        n = len(sigs)
+        if n == 0 or len(msgs) != n or len(pks) != n:
+            return G.VERIFY_FAIL
+        if any(len(m) != 32 for m in msgs) or any(len(s) != 96 for s in sigs):
+            raise ValueError("messages must be 32-byte signing roots and signatures 96 bytes")
+        if randoms is None:
+            randoms = [secrets.randbits(64) or 1 for _ in range(n)]
+        L = G.lib()
+        st = G.i32_array(n)
+        return L.gbls_multi_verify_compressed(G.buf(b"".join(msgs)), G.buf(b"".join(sigs)),
+                                              G.buf(b"".join(p.raw for p in pks)), None, None,
+                                              G.u64_array(randoms), n, st)
+
     def __eq__(self, other):
         return isinstance(other, Signature) and self.raw == other.raw
 

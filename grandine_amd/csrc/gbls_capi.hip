@@ -133,7 +133,12 @@ struct Ctx {
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
   Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, gpart, lines, Ts, V0, V1, tab, part, err, out0,
-      out1, pks, pre, pre2, msm;
+      out1, pks, pre, pre2, msm, sigd, sigst;
+  // per-call option of the next pipeline_partials on this lease: compressed signatures
+  // (96 B each, device) to decompress on the signature-side stream into `sigs`, with their
+  // BLST_ERROR statuses (device) failing their segments (consumed and reset by the pipeline)
+  const uint8_t *sig_c = nullptr;
+  int32_t *sig_st = nullptr;
   void *stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
   std::vector<uint32_t> host_tab;  // table assembly, reused across calls
@@ -602,7 +607,12 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     launch_mv_g1mul(c.side1, pks, rands, N, c.P.as<g1s>());
   }
   const int32_t *pre2 = nullptr;
-  if (sig_groupcheck) {
+  if (c.sig_c) {  // MultiVerifier::finish's decompression, inside this submission
+    launch_g2_decompress(c.side2, c.sig_c, N, const_cast<g2a *>(sigs), c.sig_st);
+    pre2 = c.sig_st;
+    c.sig_c = nullptr;
+    c.sig_st = nullptr;
+  } else if (sig_groupcheck) {
     launch_g2_check(c.side2, sigs, N, c.pre2.as<int32_t>(), 0);
     pre2 = c.pre2.as<int32_t>();
   }
@@ -725,40 +735,61 @@ bool upload_pks(Ctx &c, const PkSource &host, size_t b, size_t e, hipStream_t st
 // verdicts (host) when `verdicts`, or else the Miller partial + error flag of the single
 // segment into part_host / err_host.  Enqueues only; the caller synchronises `c.own`.
 bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
-                        const PkSource &src, const uint64_t *rands, size_t b, size_t e,
-                        const uint32_t *seg, size_t nseg, int32_t *verdicts, void *part_host,
-                        int32_t *err_host) {
+                        const uint8_t *sigs_c, int32_t *sig_status, const PkSource &src,
+                        const uint64_t *rands, size_t b, size_t e, const uint32_t *seg,
+                        size_t nseg, int32_t *verdicts, void *part_host, int32_t *err_host) {
   hipStream_t st = c.own;
   size_t n = e - b;
   if (!c.begin(st)) return false;
   if (!c.upload_staged(c.in0, msgs + 32 * b, 32 * n, st) ||
-      !c.upload_staged(c.in1, sigs + b, n * sizeof(g2a), st) ||
       !c.upload_staged(c.in3, rands + b, n * 8, st))
     return false;
-  PkSource dsrc;
-  if (!upload_pks(c, src, b, e, st, &dsrc)) return false;
-  if (verdicts) {
-    if (!c.ensure(c.out1, nseg * sizeof(int32_t))) return false;
-    if (!pipeline_verdicts(c, d, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), dsrc,
-                           c.in3.as<uint64_t>(), false, n, seg, nseg, c.out1.as<int32_t>(), st))
+  const g2a *dsigs;
+  if (sigs_c) {  // compressed: decompressed on the device by the pipeline (side stream 2)
+    if (!c.upload_staged(c.in1, sigs_c + 96 * b, 96 * n, st) ||
+        !c.ensure(c.sigd, n * sizeof(g2a) + 16) || !c.ensure(c.sigst, n * 4 + 16))
       return false;
+    c.sig_c = c.in1.as<uint8_t>();
+    c.sig_st = c.sigst.as<int32_t>();
+    dsigs = c.sigd.as<g2a>();
+  } else {
+    if (!c.upload_staged(c.in1, sigs + b, n * sizeof(g2a), st)) return false;
+    dsigs = c.in1.as<g2a>();
+  }
+  PkSource dsrc;
+  if (!upload_pks(c, src, b, e, st, &dsrc)) {
+    c.sig_c = nullptr;
+    c.sig_st = nullptr;
+    return false;
+  }
+  bool ok;
+  if (verdicts)
+    ok = c.ensure(c.out1, nseg * sizeof(int32_t)) &&
+         pipeline_verdicts(c, d, c.in0.as<uint8_t>(), nullptr, dsigs, dsrc, c.in3.as<uint64_t>(),
+                           false, n, seg, nseg, c.out1.as<int32_t>(), st);
+  else
+    ok = c.ensure(c.part, sizeof(fp12)) && c.ensure(c.err, 16) &&
+         pipeline_partials(c, d, c.in0.as<uint8_t>(), nullptr, dsigs, dsrc, c.in3.as<uint64_t>(),
+                           false, n, seg, 1, 0, c.part.as<fp12>(), c.err.as<int32_t>(), st);
+  c.sig_c = nullptr;  // the option is for this call only, consumed or not
+  c.sig_st = nullptr;
+  if (!ok) return false;
+  if (verdicts) {
     HIPCHK(hipMemcpyAsync(verdicts, c.out1.p, nseg * 4, hipMemcpyDeviceToHost, st));
   } else {
-    if (!c.ensure(c.part, sizeof(fp12)) || !c.ensure(c.err, 16)) return false;
-    if (!pipeline_partials(c, d, c.in0.as<uint8_t>(), nullptr, c.in1.as<g2a>(), dsrc,
-                           c.in3.as<uint64_t>(), false, n, seg, 1, 0, c.part.as<fp12>(),
-                           c.err.as<int32_t>(), st))
-      return false;
     HIPCHK(hipMemcpyAsync(part_host, c.part.p, sizeof(fp12), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(err_host, c.err.p, 4, hipMemcpyDeviceToHost, st));
   }
+  if (sigs_c) HIPCHK(hipMemcpyAsync(sig_status + b, c.sigst.p, n * 4, hipMemcpyDeviceToHost, st));
   return true;
 }
 
-// Host-pointer batch verification over every engine device.
-bool verify_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
-                 const uint64_t *rands, size_t n, const uint32_t *seg_off, size_t nseg,
-                 int32_t *verdicts) {
+// Host-pointer batch verification over every engine device.  Signatures are points
+// (sigs) or, for MultiVerifier::finish, compressed bytes (sigs_c, 96 B each) decompressed on
+// the device with their statuses written to sig_status.
+bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, int32_t *sig_status,
+                 const PkSource &src, const uint64_t *rands, size_t n, const uint32_t *seg_off,
+                 size_t nseg, int32_t *verdicts) {
   std::shared_lock<std::shared_mutex> rl(g.reg_mu);
   const size_t ndev = g.devs.size();
   // ---- one large batch: per-device Miller partials, one final exponentiation
@@ -774,8 +805,8 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
       leases.emplace_back(new Lease(d));
       Lease &L = *leases.back();
       uint32_t seg[2] = {0, (uint32_t)(e - b)};
-      ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, src, rands, b, e, seg, 1, nullptr,
-                                        &parts[j], &errs[j]);
+      ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, sigs_c, sig_status, src, rands, b, e,
+                                        seg, 1, nullptr, &parts[j], &errs[j]);
     }
     for (auto &L : leases)
       if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
@@ -816,8 +847,8 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
     Device &d = k == 1 ? pick_device() : *g.devs[j];
     leases.emplace_back(new Lease(d));
     Lease &L = *leases.back();
-    ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, src, rands, b, e, segs[j].data(),
-                                      s1 - s0, verdicts + s0, nullptr, nullptr);
+    ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, sigs_c, sig_status, src, rands, b, e,
+                                      segs[j].data(), s1 - s0, verdicts + s0, nullptr, nullptr);
   }
   for (auto &L : leases)
     if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
@@ -844,9 +875,11 @@ struct CoReq {
   const uint32_t *seg_off;
   size_t nseg;
   int32_t *verdicts;
+  const uint8_t *sigs_c = nullptr;  // compressed signatures instead of sigs (96 B each)
+  int32_t *sig_status = nullptr;    // their decompression statuses (with sigs_c)
   bool done = false, ok = false;
   int err = GBLS_ERR_NONE;
-  int kind() const { return (src.pts ? 1 : 0) | (src.off ? 2 : 0); }
+  int kind() const { return (src.pts ? 1 : 0) | (src.off ? 2 : 0) | (sigs_c ? 4 : 0); }
   size_t nkeys() const { return src.off ? src.off[n] : n; }
 };
 
@@ -857,14 +890,15 @@ struct Coalescer {
   int leaders = 0;
 } co;
 
-bool verify_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
-                 const uint64_t *rands, size_t n, const uint32_t *seg_off, size_t nseg,
-                 int32_t *verdicts);
+bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, int32_t *sig_status,
+                 const PkSource &src, const uint64_t *rands, size_t n, const uint32_t *seg_off,
+                 size_t nseg, int32_t *verdicts);
 
 void run_merged(std::vector<CoReq *> &batch) {
   if (batch.size() == 1) {
     CoReq &r = *batch[0];
-    r.ok = verify_host(r.msgs, r.sigs, r.src, r.rands, r.n, r.seg_off, r.nseg, r.verdicts);
+    r.ok = verify_host(r.msgs, r.sigs, r.sigs_c, r.sig_status, r.src, r.rands, r.n, r.seg_off,
+                       r.nseg, r.verdicts);
     r.err = t_last_error;
     r.done = true;
     return;
@@ -876,8 +910,9 @@ void run_merged(std::vector<CoReq *> &batch) {
     nk += r->nkeys();
   }
   const CoReq &r0 = *batch[0];
-  std::vector<uint8_t> msgs(32 * n);
-  std::vector<g2a> sigs(n);
+  std::vector<uint8_t> msgs(32 * n), sigc(r0.sigs_c ? 96 * n : 0);
+  std::vector<g2a> sigs(r0.sigs_c ? 0 : n);
+  std::vector<int32_t> sst(r0.sigs_c ? n : 0, GBLS_BAD_ENCODING);
   std::vector<uint64_t> rands(n);
   std::vector<g1a> pts;
   std::vector<uint32_t> idx, off, seg(nseg + 1);
@@ -889,7 +924,10 @@ void run_merged(std::vector<CoReq *> &batch) {
   seg[0] = 0;
   for (CoReq *r : batch) {
     std::memcpy(&msgs[32 * at], r->msgs, 32 * r->n);
-    std::memcpy(&sigs[at], r->sigs, r->n * sizeof(g2a));
+    if (r0.sigs_c)
+      std::memcpy(&sigc[96 * at], r->sigs_c, 96 * r->n);
+    else
+      std::memcpy(&sigs[at], r->sigs, r->n * sizeof(g2a));
     std::memcpy(&rands[at], r->rands, r->n * 8);
     size_t k = r->nkeys();
     if (r0.src.pts) std::memcpy(&pts[kat], r->src.pts, k * sizeof(g1a));
@@ -905,12 +943,17 @@ void run_merged(std::vector<CoReq *> &batch) {
   if (r0.src.pts) src.pts = pts.data();
   else src.idx = idx.data();
   if (r0.src.off) src.off = off.data();
-  bool ok = verify_host(msgs.data(), sigs.data(), src, rands.data(), n, seg.data(), nseg, v.data());
+  bool ok = verify_host(msgs.data(), r0.sigs_c ? nullptr : sigs.data(),
+                        r0.sigs_c ? sigc.data() : nullptr, r0.sigs_c ? sst.data() : nullptr, src,
+                        rands.data(), n, seg.data(), nseg, v.data());
   int err = t_last_error;
   sat = 0;
+  at = 0;
   for (CoReq *r : batch) {
     std::memcpy(r->verdicts, &v[sat], r->nseg * 4);
+    if (r0.sigs_c) std::memcpy(r->sig_status, &sst[at], r->n * 4);
     sat += r->nseg;
+    at += r->n;
     r->ok = ok;
     r->err = err;
     r->done = true;
@@ -919,7 +962,8 @@ void run_merged(std::vector<CoReq *> &batch) {
 
 bool coalesced_verify(CoReq &r) {
   if (!g.coalesce.load()) {
-    bool ok = verify_host(r.msgs, r.sigs, r.src, r.rands, r.n, r.seg_off, r.nseg, r.verdicts);
+    bool ok = verify_host(r.msgs, r.sigs, r.sigs_c, r.sig_status, r.src, r.rands, r.n, r.seg_off,
+                          r.nseg, r.verdicts);
     return ok;
   }
   const int max_leaders = kLeadersPerDevice * (int)g.devs.size();
@@ -1012,8 +1056,8 @@ bool bisect_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
       if (src.off) s2.off = go.data();
     }
     std::vector<int32_t> v(pieces.size(), FAILED);
-    if (!verify_host(gm.data(), gs.data(), s2, gr.data(), gs.size(), seg.data(), pieces.size(),
-                     v.data()))
+    if (!verify_host(gm.data(), gs.data(), nullptr, nullptr, s2, gr.data(), gs.size(), seg.data(),
+                     pieces.size(), v.data()))
       return false;
     frontier.clear();
     for (size_t j = 0; j < pieces.size(); j++) {
@@ -1339,6 +1383,32 @@ int gbls_multi_verify_indexed(const uint8_t (*msgs)[32], const gbls_p2_affine *s
   r.src.idx = pk_idx;
   r.src.off = pk_off;
   if (!coalesced_verify(r)) return GBLS_VERIFY_FAIL;
+  return v;
+}
+
+int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
+                                 const gbls_p1_affine *pks, const uint32_t *pk_idx,
+                                 const uint32_t *pk_off, const uint64_t *rands, size_t n,
+                                 int32_t *sig_status) {
+  fill(sig_status, n, GBLS_BAD_ENCODING);
+  API_BEGIN
+  if (n == 0) return GBLS_VERIFY_FAIL;
+  if (!pks == !pk_idx || (pks && pk_off)) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
+  if (pk_off && !valid_offsets(pk_off, n, pk_off[n])) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
+  uint32_t off[2] = {0, (uint32_t)n};
+  int32_t v = GBLS_VERIFY_FAIL;
+  CoReq r{&msgs[0][0], nullptr, PkSource(), rands, n, off, 1, &v};
+  r.src.pts = reinterpret_cast<const g1a *>(pks);
+  r.src.idx = pk_idx;
+  r.src.off = pk_off;
+  r.sigs_c = &sigs[0][0];
+  r.sig_status = sig_status;
+  if (!coalesced_verify(r)) {
+    fill(sig_status, n, GBLS_BAD_ENCODING);
+    return GBLS_VERIFY_FAIL;
+  }
+  for (size_t i = 0; i < n; i++)  // MultiVerifier::finish: a decoding error comes first
+    if (sig_status[i] != GBLS_SUCCESS) return sig_status[i];
   return v;
 }
 

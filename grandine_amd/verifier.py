@@ -168,14 +168,13 @@ class MultiVerifier(Verifier):
         """verifier.rs:301-323."""
         if not self.triples:
             return None
-        decoded = bls.decompress_signatures([t.signature_bytes for t in self.triples])
-        for st, _ in decoded:
-            if st != 0:
-                raise bls.DecompressionFailed(st)
-        signatures = [bls.Signature(raw) for _, raw in decoded]
-        ok = bls.Signature.multi_verify([t.message for t in self.triples], signatures,
-                                        [t.public_key for t in self.triples], randoms)
-        if not ok:
+        # decompression (verifier.rs:309-313) and multi_verify in one device submission
+        rc = bls.Signature.multi_verify_compressed([t.message for t in self.triples],
+                                                   [t.signature_bytes for t in self.triples],
+                                                   [t.public_key for t in self.triples], randoms)
+        if rc not in (0, 5):
+            raise bls.DecompressionFailed(rc)
+        if rc != 0:
             raise SignatureInvalid(SignatureKind.Multi)
         return None
 

@@ -25,6 +25,8 @@
  *                               bls/src/cached_public_key.rs:104-108 (Validator.pubkey,
  *                               types/src/phase0/containers.rs:229), device-resident
  *   gbls_multi_verify_indexed   multi_verify / Triple::verify_aggregate over registry indices
+ *   gbls_multi_verify_compressed  MultiVerifier::finish in one submission: signature
+ *                               decompression (verifier.rs:309-313) fused into the batch verify
  *   gbls_g1_aggregate_indexed   AggregatePublicKey::aggregate over registry indices (e.g. the
  *                               512-key get_next_sync_committee aggregate,
  *                               helper_functions/src/accessors.rs:605-628)
@@ -174,6 +176,17 @@ int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *
 int gbls_multi_verify_indexed(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
                               const uint32_t *pk_idx, const uint32_t *pk_off,
                               const uint64_t *rands, size_t n);
+/* a2, MultiVerifier::finish (helper_functions/src/verifier.rs:301-323) as ONE submission:
+ * the 96-byte compressed signatures are decompressed on the device (a8 semantics, status
+ * per signature in sig_status) on the signature-side stream while hash_to_G2 runs, then
+ * multi_verify.  Keys: pks (points), or registry indices pk_idx (+ pk_off aggregates) as
+ * in gbls_multi_verify_indexed; exactly one of pks / pk_idx.  Returns the first nonzero
+ * decompression status if any (finish's Err(DecompressionFailed), checked before the
+ * verdict), else GBLS_SUCCESS / GBLS_VERIFY_FAIL. */
+int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
+                                 const gbls_p1_affine *pks, const uint32_t *pk_idx,
+                                 const uint32_t *pk_off, const uint64_t *rands, size_t n,
+                                 int32_t *sig_status);
 /* f2: per-set verdicts (GBLS_SUCCESS / GBLS_VERIFY_FAIL, as each set would fare in
  * multi_verify alone) by GPU bisection: the batch, then rounds that split every failing
  * range 16 ways and verify all pieces as segments of one submission.  Keys come from

@@ -421,3 +421,70 @@ def test_c3_sync_committee_fav_512x10000(G, L, F, REF, registry):
     for i in list(range(0, m, 997)) + invalid[:6]:
         ref = REF.ref_verify(sigs[192 * i:192 * i + 192], msgs[32 * i:32 * i + 32], 32, pts)
         assert bool(ref) == (v[i] == 0), i
+
+
+# ------------------------------------------------------------------ fused MultiVerifier::finish
+def test_multi_verify_compressed_golden_and_decode_errors(G, L, F):
+    """gbls_multi_verify_compressed (decompression on the device inside the multi_verify
+    submission) gives every golden multi_verify verdict from the 96-byte signatures, and a
+    signature that fails to decode returns its BLST_ERROR status (finish's
+    Err(DecompressionFailed)) with the per-signature statuses, before any verdict."""
+    from grandine_amd import bls as B
+    with open(os.path.join(ROOT, "tests", "golden", "multi_verify.json")) as fh:
+        cases = json.load(fh)["cases"]
+    for c in cases:
+        msgs = [bytes.fromhex(h) for h in c["msgs"]]
+        if not msgs or any(len(m) != 32 for m in msgs):
+            continue
+        pks = []
+        for h in c["pks"]:
+            if h == "c0" + "00" * 47:
+                pks.append(B.PublicKey.default())
+            else:
+                st, raw = B.decompress_public_keys([bytes.fromhex(h)], validate=False)[0]
+                pks.append(B.PublicKey(raw))
+        rc = B.Signature.multi_verify_compressed(msgs, [bytes.fromhex(h) for h in c["sigs"]], pks,
+                                                 [int(r) for r in c["rands"]])
+        assert (rc == G.SUCCESS) == c["expect"], c.get("note")  # undecodable: its status
+    n = 64
+    msgs, sigs, pks, rands = F.c2_batch(n, seed=77)
+    comp = ctypes.create_string_buffer(96 * n)
+    G.check(L.gbls_g2_compress(sigs, n, comp), "compress")
+    st = G.i32_array(n)
+    r64 = (ctypes.c_uint64 * n)(*rands)
+    assert L.gbls_multi_verify_compressed(msgs, comp, pks, None, None, r64, n, st) == G.SUCCESS
+    assert list(st) == [0] * n
+    bad = bytearray(comp.raw)
+    bad[96 * 17] &= 0x7F  # clear the compression flag: BAD_ENCODING
+    rc = L.gbls_multi_verify_compressed(msgs, bytes(bad), pks, None, None, r64, n, st)
+    assert rc == G.BAD_ENCODING and st[17] == G.BAD_ENCODING
+    assert [s for i, s in enumerate(st) if i != 17] == [0] * (n - 1)
+    swapped = bytearray(comp.raw)
+    swapped[96 * 3:96 * 4], swapped[96 * 4:96 * 5] = comp.raw[96 * 4:96 * 5], comp.raw[96 * 3:96 * 4]
+    assert L.gbls_multi_verify_compressed(msgs, bytes(swapped), pks, None, None, r64, n, st) == G.VERIFY_FAIL
+    # exactly one key source
+    assert L.gbls_multi_verify_compressed(msgs, comp, None, None, None, r64, n, st) == G.VERIFY_FAIL
+
+
+def test_multi_verify_compressed_block_shape(G, L, F, registry):
+    """C1 shape through the fused entry: 131 sets whose keys are registry aggregates (1, 1,
+    128 x 512, 512 keys), equal to decompress + gbls_multi_verify_indexed, and rejecting a
+    swapped signature pair."""
+    sks, comp_keys = registry
+    rng = np.random.default_rng(9)
+    sizes = [1, 1] + [512] * 128 + [512]
+    idx = np.concatenate([rng.choice(N_REG, size=s, replace=False) for s in sizes]).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    n = len(sizes)
+    msgs = F.messages(n, b"c1-test")
+    sigs, _ = F.committee_signatures(sks, idx, off, msgs)
+    comp = ctypes.create_string_buffer(96 * n)
+    G.check(L.gbls_g2_compress(sigs, n, comp), "compress")
+    rands = (ctypes.c_uint64 * n)(*F.rands(n, 9))
+    pidx, poff = idx.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p)
+    st = G.i32_array(n)
+    assert L.gbls_multi_verify_compressed(msgs, comp, None, pidx, poff, rands, n, st) == G.SUCCESS
+    assert L.gbls_multi_verify_indexed(msgs, sigs, pidx, poff, rands, n) == G.SUCCESS
+    bad = bytearray(comp.raw)
+    bad[96 * 40:96 * 41], bad[96 * 41:96 * 42] = comp.raw[96 * 41:96 * 42], comp.raw[96 * 40:96 * 41]
+    assert L.gbls_multi_verify_compressed(msgs, bytes(bad), None, pidx, poff, rands, n, st) == G.VERIFY_FAIL
