@@ -608,6 +608,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   }
   const int32_t *pre2 = nullptr;
   if (c.sig_c) {  // MultiVerifier::finish's decompression, inside this submission
+    // sigs is then the lease's own output buffer (c.sigd, enqueue_host_batch)
     launch_g2_decompress(c.side2, c.sig_c, N, const_cast<g2a *>(sigs), c.sig_st);
     pre2 = c.sig_st;
     c.sig_c = nullptr;
@@ -1390,6 +1391,7 @@ int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs
                                  const gbls_p1_affine *pks, const uint32_t *pk_idx,
                                  const uint32_t *pk_off, const uint64_t *rands, size_t n,
                                  int32_t *sig_status) {
+  if (!sig_status) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
   fill(sig_status, n, GBLS_BAD_ENCODING);
   API_BEGIN
   if (n == 0) return GBLS_VERIFY_FAIL;
