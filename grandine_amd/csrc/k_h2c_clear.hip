@@ -95,7 +95,7 @@ void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   if (!n) return;
   if (n >= kLaneRegimeClear)
     k_h2c_clear_lane<<<nblk(n), WG, 0, st>>>(Q, n, H);
-  else if (n <= kRowClearMax)
+  else if (n <= g_row_clear_max)
     k_h2c_clear_row<<<nblk((size_t)n * 16), WG, 0, st>>>(Q, n, H);
   else
     k_h2c_clear<<<nblk((size_t)n * 4), WG, 0, st>>>(Q, n, H);
