@@ -23,7 +23,7 @@ constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
 // ... and Miller lines of up to this many pairs run on 16-lane DPP rows (bls_gang.h),
 // 16 x 4096 lanes being one wave per SIMD
 constexpr uint32_t kRowRegimeMax = 6144;
-constexpr uint32_t kRowClearMax = 1024;  // cofactor clearing on rows (tiny launches only)
+constexpr uint32_t kRowClearMax = 4096;  // cofactor clearing on rows (up to one C2 batch)
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
 // line-coefficient buffer bound per submission (19.6 KB per pair: 4 GB = 214k pairs,
 // a C5 shard of 131 072 sets unsliced; tiny next to 288 GB of HBM): above it the Miller
