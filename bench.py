@@ -31,7 +31,7 @@ in total), C3 needs no exchange (per-message verdicts).
 
 Extra JSON fields: "roofline" (dominant kernel's integer-multiply throughput vs the
 measured v_mad_u64_u32 peak, HIP events on the launch stream, W frozen in BASELINE.md 4)
-and "cpu_baseline" (the C oracle, a TEXTBOOK restatement of blst's multi-verify, timed on
+and "cpu_baseline" (the C restatement of blst's multi-verify built with BLS_REF_FAST, timed on
 this host's cores).
 """
 
@@ -103,9 +103,9 @@ def pmc_traffic(kernel, default_cmd):
 
 
 def cpu_baseline(n_sample, threads):
-    """Time the C oracle (oracle/_build/bls_ref_bench) on a bounded sample of the C2
-    workload shape; None if the oracle is not built."""
-    exe = os.path.join(ROOT, "oracle", "_build", "bls_ref_bench")
+    """Time the C port (oracle/_build/bls_ref_bench_fast: oracle/bls_ref.c with BLS_REF_FAST) on
+    a bounded sample of the C2 workload shape; None if it is not built."""
+    exe = os.path.join(ROOT, "oracle", "_build", "bls_ref_bench_fast")
     if not os.path.exists(exe):
         return None
     try:
@@ -115,10 +115,11 @@ def cpu_baseline(n_sample, threads):
     except Exception as e:  # noqa: BLE001 -- report, never fake a number
         return {"value": None, "unit": "sets/s", "cores": threads, "kind": "port", "error": str(e)[:200]}
     return {"value": rec["sets_per_s"], "unit": "sets/s", "cores": threads, "kind": "port",
-            "sample": "%d-set multi_verify batch, %d threads: oracle/bls_ref.c, a TEXTBOOK C restatement of "
-                      "blst's multi-verify algorithm (schoolbook Fp2/Fp6, Fermat inversion, plain 1269-bit "
-                      "hard part; no w5 windows / Karatsuba / cyclotomic squaring), so it understates "
-                      "rayon+blst" % (n_sample, threads),
+            "sample": "%d-set multi_verify batch, %d threads: oracle/bls_ref.c built with BLS_REF_FAST, a C "
+                      "restatement of blst's multi-verify algorithm (Karatsuba Fp2/Fp6/Fp12, complex "
+                      "squarings, 4-bit windowed exponentiations; portable C with 64-bit limbs, Fermat "
+                      "inversion, plain 1269-bit hard part, no assembly / cyclotomic squaring), so it still "
+                      "understates rayon+blst" % (n_sample, threads),
             "verdict_ok": rec.get("ok")}
 
 

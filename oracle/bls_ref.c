@@ -130,12 +130,26 @@ static void fe_from_u64(fe *r, u64 x) {
 }
 /* a^e, e given as 6 little-endian words */
 static void fe_pow(fe *r, const fe *a, const u64 *e) {
+#ifdef BLS_REF_FAST /* fixed 4-bit windows: 384 squarings + 96 + 14 products */
+  fe tab[16];
+  tab[0] = ONE;
+  tab[1] = *a;
+  for (int i = 2; i < 16; i++) fe_mul(&tab[i], &tab[i - 1], a);
+  fe acc = ONE;
+  for (int i = 380; i >= 0; i -= 4) {
+    for (int k = 0; k < 4; k++) fe_sqr(&acc, &acc);
+    unsigned d = (unsigned)((e[i >> 6] >> (i & 63)) & 15);
+    if (d) fe_mul(&acc, &acc, &tab[d]);
+  }
+  *r = acc;
+#else
   fe acc = ONE;
   for (int i = 383; i >= 0; i--) {
     fe_sqr(&acc, &acc);
     if ((e[i >> 6] >> (i & 63)) & 1) fe_mul(&acc, &acc, a);
   }
   *r = acc;
+#endif
 }
 static u64 E_PM2[6], E_SQRT[6], E_LEG[6], E_PM3D4[6], E_PM1D2[6];
 static void fe_inv(fe *r, const fe *a) { fe_pow(r, a, E_PM2); }
@@ -176,6 +190,27 @@ static void fe2_add(fe2 *r, const fe2 *a, const fe2 *b) { fe_add(&r->a, &a->a, &
 static void fe2_sub(fe2 *r, const fe2 *a, const fe2 *b) { fe_sub(&r->a, &a->a, &b->a); fe_sub(&r->b, &a->b, &b->b); }
 static void fe2_neg(fe2 *r, const fe2 *a) { fe_neg(&r->a, &a->a); fe_neg(&r->b, &a->b); }
 static void fe2_conj(fe2 *r, const fe2 *a) { r->a = a->a; fe_neg(&r->b, &a->b); }
+#ifdef BLS_REF_FAST /* Karatsuba product (3 Fp products), complex squaring (2) */
+static void fe2_mul(fe2 *r, const fe2 *a, const fe2 *b) {
+  fe t0, t1, sa, sb;
+  fe_mul(&t0, &a->a, &b->a);
+  fe_mul(&t1, &a->b, &b->b);
+  fe_add(&sa, &a->a, &a->b);
+  fe_add(&sb, &b->a, &b->b);
+  fe_mul(&sa, &sa, &sb);
+  fe_sub(&r->a, &t0, &t1);
+  fe_add(&t0, &t0, &t1);
+  fe_sub(&r->b, &sa, &t0);
+}
+static void fe2_sqr(fe2 *r, const fe2 *a) {
+  fe s, d, m;
+  fe_add(&s, &a->a, &a->b);
+  fe_sub(&d, &a->a, &a->b);
+  fe_mul(&m, &a->a, &a->b);
+  fe_mul(&r->a, &s, &d);
+  fe_add(&r->b, &m, &m);
+}
+#else
 static void fe2_mul(fe2 *r, const fe2 *a, const fe2 *b) { /* schoolbook */
   fe t0, t1, t2, t3;
   fe_mul(&t0, &a->a, &b->a);
@@ -186,6 +221,7 @@ static void fe2_mul(fe2 *r, const fe2 *a, const fe2 *b) { /* schoolbook */
   fe_add(&r->b, &t2, &t3);
 }
 static void fe2_sqr(fe2 *r, const fe2 *a) { fe2_mul(r, a, a); }
+#endif
 static void fe2_mul_fe(fe2 *r, const fe2 *a, const fe *b) { fe_mul(&r->a, &a->a, b); fe_mul(&r->b, &a->b, b); }
 static void fe2_mul_xi(fe2 *r, const fe2 *a) { /* (1+u) a */
   fe t0, t1;
@@ -205,12 +241,26 @@ static void fe2_inv(fe2 *r, const fe2 *a) {
   fe_neg(&r->b, &t);
 }
 static void fe2_pow(fe2 *r, const fe2 *a, const u64 *e) {
+#ifdef BLS_REF_FAST /* fixed 4-bit windows */
+  fe2 tab[16];
+  tab[0] = F2ONE;
+  tab[1] = *a;
+  for (int i = 2; i < 16; i++) fe2_mul(&tab[i], &tab[i - 1], a);
+  fe2 acc = F2ONE;
+  for (int i = 380; i >= 0; i -= 4) {
+    for (int k = 0; k < 4; k++) fe2_sqr(&acc, &acc);
+    unsigned d = (unsigned)((e[i >> 6] >> (i & 63)) & 15);
+    if (d) fe2_mul(&acc, &acc, &tab[d]);
+  }
+  *r = acc;
+#else
   fe2 acc = F2ONE;
   for (int i = 383; i >= 0; i--) {
     fe2_sqr(&acc, &acc);
     if ((e[i >> 6] >> (i & 63)) & 1) fe2_mul(&acc, &acc, a);
   }
   *r = acc;
+#endif
 }
 static int fe2_is_square(const fe2 *a) {
   fe n, t;
@@ -252,6 +302,22 @@ static int fe2_lex_largest(const fe2 *a) {
 static void fe6_add(fe6 *r, const fe6 *a, const fe6 *b) { for (int i = 0; i < 3; i++) fe2_add(&r->c[i], &a->c[i], &b->c[i]); }
 static void fe6_sub(fe6 *r, const fe6 *a, const fe6 *b) { for (int i = 0; i < 3; i++) fe2_sub(&r->c[i], &a->c[i], &b->c[i]); }
 static void fe6_neg(fe6 *r, const fe6 *a) { for (int i = 0; i < 3; i++) fe2_neg(&r->c[i], &a->c[i]); }
+static void fe6_mul_v(fe6 *r, const fe6 *a);
+#ifdef BLS_REF_FAST /* Karatsuba over Fp2: 6 products, v^3 = xi */
+static void fe6_mul(fe6 *r, const fe6 *a, const fe6 *b) {
+  fe2 v0, v1, v2, t, u, c0, c1, c2;
+  fe2_mul(&v0, &a->c[0], &b->c[0]);
+  fe2_mul(&v1, &a->c[1], &b->c[1]);
+  fe2_mul(&v2, &a->c[2], &b->c[2]);
+  fe2_add(&t, &a->c[1], &a->c[2]); fe2_add(&u, &b->c[1], &b->c[2]); fe2_mul(&t, &t, &u);
+  fe2_sub(&t, &t, &v1); fe2_sub(&t, &t, &v2); fe2_mul_xi(&t, &t); fe2_add(&c0, &t, &v0);
+  fe2_add(&t, &a->c[0], &a->c[1]); fe2_add(&u, &b->c[0], &b->c[1]); fe2_mul(&t, &t, &u);
+  fe2_sub(&t, &t, &v0); fe2_sub(&t, &t, &v1); fe2_mul_xi(&u, &v2); fe2_add(&c1, &t, &u);
+  fe2_add(&t, &a->c[0], &a->c[2]); fe2_add(&u, &b->c[0], &b->c[2]); fe2_mul(&t, &t, &u);
+  fe2_sub(&t, &t, &v0); fe2_sub(&t, &t, &v2); fe2_add(&c2, &t, &v1);
+  r->c[0] = c0; r->c[1] = c1; r->c[2] = c2;
+}
+#else
 static void fe6_mul(fe6 *r, const fe6 *a, const fe6 *b) { /* schoolbook, v^3 = xi */
   fe2 acc[5], t;
   for (int k = 0; k < 5; k++) acc[k] = F2ZERO;
@@ -266,6 +332,7 @@ static void fe6_mul(fe6 *r, const fe6 *a, const fe6 *b) { /* schoolbook, v^3 = x
   fe2_add(&r->c[1], &acc[1], &t);
   r->c[2] = acc[2];
 }
+#endif
 static void fe6_mul_v(fe6 *r, const fe6 *a) {
   fe2 t;
   fe2_mul_xi(&t, &a->c[2]);
@@ -284,6 +351,32 @@ static void fe6_inv(fe6 *r, const fe6 *a) {
   fe2_mul(&r->c[0], &c0, &t); fe2_mul(&r->c[1], &c1, &t); fe2_mul(&r->c[2], &c2, &t);
 }
 static fe12 F12ONE;
+#ifdef BLS_REF_FAST /* Karatsuba over Fp6 (3 products), complex squaring (2 products) */
+static void fe12_mul(fe12 *r, const fe12 *a, const fe12 *b) {
+  fe6 t0, t1, s, u;
+  fe6_mul(&t0, &a->c[0], &b->c[0]);
+  fe6_mul(&t1, &a->c[1], &b->c[1]);
+  fe6_add(&s, &a->c[0], &a->c[1]);
+  fe6_add(&u, &b->c[0], &b->c[1]);
+  fe6_mul(&s, &s, &u);
+  fe6_sub(&s, &s, &t0);
+  fe6_sub(&r->c[1], &s, &t1);
+  fe6_mul_v(&t1, &t1);
+  fe6_add(&r->c[0], &t0, &t1);
+}
+static void fe12_sqr(fe12 *r, const fe12 *a) { /* (a0 + a1 w)^2, w^2 = v */
+  fe6 m, s, t, u;
+  fe6_mul(&m, &a->c[0], &a->c[1]);
+  fe6_add(&s, &a->c[0], &a->c[1]);
+  fe6_mul_v(&t, &a->c[1]);
+  fe6_add(&t, &t, &a->c[0]);
+  fe6_mul(&s, &s, &t);          /* (a0 + a1)(a0 + v a1) = a0^2 + v a1^2 + (1 + v) m */
+  fe6_sub(&s, &s, &m);
+  fe6_mul_v(&u, &m);
+  fe6_sub(&r->c[0], &s, &u);    /* a0^2 + v a1^2 */
+  fe6_add(&r->c[1], &m, &m);    /* 2 a0 a1 */
+}
+#else
 static void fe12_mul(fe12 *r, const fe12 *a, const fe12 *b) {
   fe6 t0, t1, t2, t3;
   fe6_mul(&t0, &a->c[0], &b->c[0]);
@@ -295,6 +388,7 @@ static void fe12_mul(fe12 *r, const fe12 *a, const fe12 *b) {
   fe6_add(&r->c[1], &t2, &t3);
 }
 static void fe12_sqr(fe12 *r, const fe12 *a) { fe12_mul(r, a, a); }
+#endif
 static void fe12_conj(fe12 *r, const fe12 *a) { r->c[0] = a->c[0]; fe6_neg(&r->c[1], &a->c[1]); }
 static void fe12_inv(fe12 *r, const fe12 *a) {
   fe6 t0, t1;
