@@ -1,0 +1,234 @@
+// Radix-2^28 arithmetic over the BLS12-381 base field: the next field layer, not yet used by the
+// kernels (tools/ubench/r28_bench.hip measured its product at 1.40x the
+// engine's product per lane on MI355X).
+//
+// An element is 14 limbs of 28 bits in Montgomery form with R = 2^392.  A column of the
+// product-scanning Montgomery product holds at most 28 terms (42 for a dual product), so with
+// limbs < 2^29 every term is < 2^58 and the column fits one 64-bit accumulator: one
+// v_mad_u64_u32 per term and no carry word (the engine's 32-bit limbs need a mad + addc pair).
+// R/p ~ 2^11.3, so the REDC bound T < R p holds for inputs up to ~35 p (dual) and outputs are
+// < p (1 + T / (R p)) ~ 1.01 p: no final subtraction.
+//
+// Limb and value contract:
+//   normalized: every limb < 2^28 (outputs of mul, mul2, norm, sub, from_fp);
+//   mul/mul2 inputs: limbs < 2^29 (one add_lazy of two normalized elements), values < 32 p;
+//   sub(a, b) = norm(4p + a - b) needs b normalized and < 4p + a (4p is stored with every limb
+//   but the top in [2^28 - 1, 2^29), so no lower limb borrows; the top limb wraps back);
+//   neg_lazy(a) = 4p - a needs a < 2p.
+// canon() gives the unique representative in [0, p) (values < 16 p).
+#pragma once
+
+#include "bls_field.h"
+
+namespace gbls {
+namespace r28 {
+
+struct fe {
+  uint32_t l[14];
+};
+struct fe2 {
+  fe c0, c1;
+};
+
+constexpr uint32_t kMask = 0x0fffffff;
+constexpr uint32_t kPinv = 0x0ffcfffd;  // -p^-1 mod 2^28
+
+#define GBLS_R28_P                                                                              \
+  0xfffaaab, 0xfefffff, 0x3ffffb9, 0xfffeb15, 0x6241eab, 0xa0f6b0f, 0xf6730d2, 0xf38512b,        \
+      0x4774b84, 0x4bacd76, 0xba7b643, 0xe69a4b1, 0x1ea397f, 0x1a011
+// 4p, every limb but the top rebalanced into [2^28 - 1, 2^29)
+#define GBLS_R28_BIAS4P                                                                         \
+  0x1ffeaaac, 0x1fbffffe, 0x1ffffee6, 0x1fffac53, 0x18907aae, 0x183dac3c, 0x1d9cc349,            \
+      0x1ce144ae, 0x11dd2e12, 0x12eb35d8, 0x1e9ed90c, 0x19a692c5, 0x17a8e5fe, 0x68043
+// 2^400 mod p: x 2^384 (engine form) times this, over R = 2^392, is x 2^392
+#define GBLS_R28_CIN                                                                            \
+  0x80e6299, 0x3500034, 0xeb12856, 0xdeb2699, 0xc988670, 0x4ef6697, 0x70983e8, 0xa4e6fe9,        \
+      0x3e8a053, 0xecf271e, 0xc20d323, 0x6eb6385, 0x47f1286, 0x156da
+// 2^384 mod p: x 2^392 times this, over R, is x 2^384
+#define GBLS_R28_COUT                                                                           \
+  0x2fffd, 0x900000, 0xc000276, 0xbc40, 0x8baebf4, 0x5753c75, 0x55f4898, 0x7052574, 0x7ce5853,   \
+      0x56ec6d7, 0x71a97a2, 0xe4935c0, 0xec3fa80, 0x15f65
+
+// (sum over the NP pairs x_k y_k) / 2^392 mod p, product scanning
+template <int NP>
+HD void mul_n(fe &r, const fe *const *x, const fe *const *y) {
+  constexpr uint32_t P[14] = {GBLS_R28_P};
+  uint32_t m[14], t[14];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 14) {
+#pragma unroll
+        for (int q = 0; q < NP; q++) acc += (uint64_t)x[q]->l[i] * y[q]->l[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (i < k && j >= 0 && j < 14) acc += (uint64_t)m[i] * P[j];
+    }
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * kPinv) & kMask;
+      acc += (uint64_t)m[k] * P[0];
+    } else {
+      t[k - 14] = (uint32_t)acc & kMask;
+    }
+    acc >>= 28;
+  }
+  t[13] = (uint32_t)acc;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = t[i];
+}
+HD void mul(fe &r, const fe &a, const fe &b) {
+  const fe *x[1] = {&a}, *y[1] = {&b};
+  mul_n<1>(r, x, y);
+}
+// a b + c d in one reduction
+HD void mul2(fe &r, const fe &a, const fe &b, const fe &c, const fe &d) {
+  const fe *x[2] = {&a, &c}, *y[2] = {&b, &d};
+  mul_n<2>(r, x, y);
+}
+
+HD void norm(fe &a) {
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    a.l[i + 1] += a.l[i] >> 28;
+    a.l[i] &= kMask;
+  }
+}
+// limbwise, no carries: limbs < 2^29 from normalized inputs (a product operand)
+HD void add_lazy(fe &r, const fe &a, const fe &b) {
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = a.l[i] + b.l[i];
+}
+HD void add(fe &r, const fe &a, const fe &b) {
+  add_lazy(r, a, b);
+  norm(r);
+}
+// 4p + a - b, normalized (b < 4p, normalized)
+HD void sub(fe &r, const fe &a, const fe &b) {
+  constexpr uint32_t B[14] = {GBLS_R28_BIAS4P};
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = B[i] + a.l[i] - b.l[i];
+  norm(r);
+}
+// 4p - a (a < 2p, normalized): limbs < 2^29, a product operand without normalization
+HD void neg_lazy(fe &r, const fe &a) {
+  constexpr uint32_t B[14] = {GBLS_R28_BIAS4P};
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = B[i] - a.l[i];
+}
+
+// a - p if a >= p (a normalized); returns 1 if it subtracted
+HD uint32_t sub_p_if_geq(fe &a) {
+  constexpr uint32_t P[14] = {GBLS_R28_P};
+  fe d;
+  int32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    int32_t v = (int32_t)a.l[i] - (int32_t)P[i] + borrow;
+    borrow = v >> 28;  // 0 or -1 (arithmetic shift)
+    d.l[i] = (uint32_t)v & kMask;
+  }
+  const uint32_t ge = borrow == 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) a.l[i] = ge ? d.l[i] : a.l[i];
+  return ge;
+}
+// the representative in [0, p) of a value < 16 p
+HD void canon(fe &a) {
+  norm(a);
+  for (int s = 0; s < 15; s++)
+    if (!sub_p_if_geq(a)) break;
+}
+HD bool is_zero(const fe &a) {
+  fe t = a;
+  canon(t);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) o |= t.l[i];
+  return o == 0;
+}
+
+// engine form (12 x 32-bit limbs, x 2^384 mod p, < 2^384) <-> radix-2^28 form (x 2^392)
+HD void repack_in(fe &r, const fp &a) {
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const int bit = 28 * i, w = bit >> 5, s = bit & 31;
+    uint32_t v = a.l[w] >> s;
+    if (s > 4 && w + 1 < 12) v |= a.l[w + 1] << (32 - s);
+    r.l[i] = v & kMask;
+  }
+}
+HD void repack_out(fp &r, const fe &a) {
+  uint64_t buf = 0;
+  int have = 0, w = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    buf |= (uint64_t)a.l[i] << have;
+    have += 28;
+    if (have >= 32 && w < 12) {
+      r.l[w++] = (uint32_t)buf;
+      buf >>= 32;
+      have -= 32;
+    }
+  }
+  if (w < 12) r.l[w] = (uint32_t)buf;
+}
+HD void from_fp(fe &r, const fp &a) {
+  constexpr fe C = {{GBLS_R28_CIN}};
+  fe t;
+  repack_in(t, a);
+  mul(r, t, C);
+}
+HD void to_fp(fp &r, const fe &a) {
+  constexpr fe C = {{GBLS_R28_COUT}};
+  fe t;
+  mul(t, a, C);
+  canon(t);
+  repack_out(r, t);
+}
+
+// ------------------------------------------------------------------ Fp2 = Fp[u] / (u^2 + 1)
+HD void fe2_mul(fe2 &r, const fe2 &a, const fe2 &b) {
+  fe nb1, c0;
+  neg_lazy(nb1, b.c1);
+  mul2(c0, a.c0, b.c0, a.c1, nb1);
+  mul2(r.c1, a.c0, b.c1, a.c1, b.c0);
+  r.c0 = c0;
+}
+// (a0 + a1)(a0 - a1), 2 a0 a1
+HD void fe2_sqr(fe2 &r, const fe2 &a) {
+  fe s, d, t;
+  add_lazy(s, a.c0, a.c1);
+  sub(d, a.c0, a.c1);
+  add_lazy(t, a.c1, a.c1);
+  mul(r.c1, a.c0, t);
+  mul(r.c0, s, d);
+}
+HD void fe2_add(fe2 &r, const fe2 &a, const fe2 &b) {
+  add(r.c0, a.c0, b.c0);
+  add(r.c1, a.c1, b.c1);
+}
+HD void fe2_sub(fe2 &r, const fe2 &a, const fe2 &b) {
+  sub(r.c0, a.c0, b.c0);
+  sub(r.c1, a.c1, b.c1);
+}
+HD void fe2_mul_fe(fe2 &r, const fe2 &a, const fe &b) {
+  mul(r.c0, a.c0, b);
+  mul(r.c1, a.c1, b);
+}
+// times xi = 1 + u
+HD void fe2_mul_xi(fe2 &r, const fe2 &a) {
+  fe t0, t1;
+  sub(t0, a.c0, a.c1);
+  add(t1, a.c0, a.c1);
+  r.c0 = t0;
+  r.c1 = t1;
+}
+
+}  // namespace r28
+}  // namespace gbls

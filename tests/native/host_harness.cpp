@@ -8,6 +8,7 @@
 #include "../../grandine_amd/csrc/bls_hash.h"
 #include "../../grandine_amd/csrc/bls_pairing.h"
 #include "../../grandine_amd/csrc/bls_wave12.h"
+#include "../../grandine_amd/csrc/bls_field28.h"
 
 using namespace gbls;
 
@@ -21,6 +22,47 @@ void h_fp_mul(const uint32_t *a, const uint32_t *b, uint32_t *r) {
   std::memcpy(y.l, b, 48);
   fp_mul(z, x, y);
   std::memcpy(r, z.l, 48);
+}
+
+// radix-2^28 layer (bls_field28.h) through the engine form: op 0 = round trip of a,
+// 1 = a b, 2 = a b + c d (mul2), 3 = a - b (sub, then mul by 1 path), 4 = Fp2 (a + b u)(c + d u)
+// into r (and r2), 5 = Fp2 square of a + b u, 6 = is_zero(a - b)
+int h_r28_op(int op, const uint32_t *a, const uint32_t *b, const uint32_t *c, const uint32_t *d,
+             uint32_t *r, uint32_t *r2) {
+  fp x[4];
+  std::memcpy(x[0].l, a, 48);
+  std::memcpy(x[1].l, b, 48);
+  std::memcpy(x[2].l, c, 48);
+  std::memcpy(x[3].l, d, 48);
+  r28::fe e[4];
+  for (int i = 0; i < 4; i++) r28::from_fp(e[i], x[i]);
+  r28::fe o;
+  r28::fe2 o2;
+  fp z, z2;
+  int ret = 0;
+  switch (op) {
+    case 0: o = e[0]; break;
+    case 1: r28::mul(o, e[0], e[1]); break;
+    case 2: r28::mul2(o, e[0], e[1], e[2], e[3]); break;
+    case 3: r28::sub(o, e[0], e[1]); break;
+    case 4:
+    case 5: {
+      r28::fe2 u = {e[0], e[1]}, v = {e[2], e[3]};
+      if (op == 4)
+        r28::fe2_mul(o2, u, v);
+      else
+        r28::fe2_sqr(o2, u);
+      o = o2.c0;
+      r28::to_fp(z2, o2.c1);
+      std::memcpy(r2, z2.l, 48);
+      break;
+    }
+    case 6: r28::sub(o, e[0], e[1]); ret = r28::is_zero(o); break;
+    default: return -1;
+  }
+  r28::to_fp(z, o);
+  std::memcpy(r, z.l, 48);
+  return ret;
 }
 
 int h_g1_decompress(const uint8_t *in, int validate, uint8_t *out96) {

@@ -182,3 +182,36 @@ def test_inversion_free_final_verdict(H):
         assert want == (trial < 3)
         assert H.h_w12_verdict(out.raw) == want
     assert H.h_w12_verdict(bytes(576)) == 0
+
+
+def test_radix28_field_layer(H):
+    """bls_field28.h (the next field layer) against Python big integers, through
+    the engine form: conversions, product, dual product, subtraction, Fp2 product/square."""
+    import random
+    rng = random.Random(28)
+    H.h_r28_op.argtypes = [ctypes.c_int] + [ctypes.c_char_p] * 4 + [ctypes.c_void_p] * 2
+    R = 1 << 384
+    m = lambda x: (x * R % O.P).to_bytes(48, "little")  # engine (Montgomery-384) form
+    edge = [0, 1, 2, O.P - 1, O.P - 2, (1 << 380), O.P // 2]
+    vals = edge + [rng.randrange(O.P) for _ in range(120)]
+    for i in range(len(vals)):
+        a, b, c, d = vals[i], vals[-1 - i], rng.choice(vals), rng.choice(vals)
+        r, r2 = ctypes.create_string_buffer(48), ctypes.create_string_buffer(48)
+
+        def run(op):
+            ret = H.h_r28_op(op, m(a), m(b), m(c), m(d), r, r2)
+            got = int.from_bytes(r.raw, "little") * RINV % O.P
+            got2 = int.from_bytes(r2.raw, "little") * RINV % O.P
+            assert int.from_bytes(r.raw, "little") < O.P  # canonical engine form
+            return ret, got, got2
+        assert run(0)[1] == a
+        assert run(1)[1] == a * b % O.P
+        assert run(2)[1] == (a * b + c * d) % O.P
+        assert run(3)[1] == (a - b) % O.P
+        _, g0, g1 = run(4)
+        assert (g0, g1) == ((a * c - b * d) % O.P, (a * d + b * c) % O.P)
+        _, g0, g1 = run(5)
+        assert (g0, g1) == ((a * a - b * b) % O.P, 2 * a * b % O.P)
+        assert run(6)[0] == (a == b)
+    r, r2 = ctypes.create_string_buffer(48), ctypes.create_string_buffer(48)
+    assert H.h_r28_op(6, m(5), m(5), m(0), m(0), r, r2) == 1
