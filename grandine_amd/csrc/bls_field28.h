@@ -40,6 +40,10 @@ constexpr uint32_t kPinv = 0x0ffcfffd;  // -p^-1 mod 2^28
 #define GBLS_R28_BIAS4P                                                                         \
   0x1ffeaaac, 0x1fbffffe, 0x1ffffee6, 0x1fffac53, 0x18907aae, 0x183dac3c, 0x1d9cc349,            \
       0x1ce144ae, 0x11dd2e12, 0x12eb35d8, 0x1e9ed90c, 0x19a692c5, 0x17a8e5fe, 0x68043
+// 8p, every limb but the top rebalanced into [2^28 - 1, 2^29)
+#define GBLS_R28_BIAS8P                                                                         \
+  0x1ffd5558, 0x1f7ffffe, 0x1ffffdce, 0x1fff58a8, 0x1120f55e, 0x107b587a, 0x1b398694,           \
+      0x19c2895e, 0x13ba5c26, 0x15d66bb1, 0x1d3db219, 0x134d258c, 0x1f51cbfe, 0xd0087
 // 2^400 mod p: x 2^384 (engine form) times this, over R = 2^392, is x 2^392
 #define GBLS_R28_CIN                                                                            \
   0x80e6299, 0x3500034, 0xeb12856, 0xdeb2699, 0xc988670, 0x4ef6697, 0x70983e8, 0xa4e6fe9,        \
@@ -79,6 +83,13 @@ HD void mul_n(fe &r, const fe *const *x, const fe *const *y) {
     acc >>= 28;
   }
   t[13] = (uint32_t)acc;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // a scheduling boundary after every product: the compiler keeps products in source order
+  // instead of interleaving independent ones (which spills; see tools/gen_fpmul.py)
+  asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]),
+               "+v"(t[6]), "+v"(t[7]), "+v"(t[8]), "+v"(t[9]), "+v"(t[10]), "+v"(t[11]),
+               "+v"(t[12]), "+v"(t[13]));
+#endif
 #pragma unroll
   for (int i = 0; i < 14; i++) r.l[i] = t[i];
 }
@@ -192,10 +203,35 @@ HD void to_fp(fp &r, const fe &a) {
   repack_out(r, t);
 }
 
+// a - q p for q = floor(top limb / (p_top + 1)) <= a / p: a normalized (< 2^392) -> < 1.03 p
+HD void wred(fe &a) {
+  constexpr uint32_t P[14] = {GBLS_R28_P};
+  const uint32_t q = a.l[13] / 0x1a012u;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    c += (int64_t)a.l[i] - (int64_t)q * P[i];
+    a.l[i] = (uint32_t)c & kMask;
+    c >>= 28;
+  }
+}
+// 8p + a - b, normalized and weakly reduced (< 1.03 p): b normalized, < 8p + a
+HD void sub_r(fe &r, const fe &a, const fe &b) {
+  constexpr uint32_t B[14] = {GBLS_R28_BIAS8P};
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = B[i] + a.l[i] - b.l[i];
+  norm(r);
+  wred(r);
+}
+
 // ------------------------------------------------------------------ Fp2 = Fp[u] / (u^2 + 1)
+// a: limbs < 2^29 (a lazy sum of normalized elements), value < 5p; b: normalized, < 5p;
+// output < 1.03 p
 HD void fe2_mul(fe2 &r, const fe2 &a, const fe2 &b) {
+  constexpr uint32_t B[14] = {GBLS_R28_BIAS8P};
   fe nb1, c0;
-  neg_lazy(nb1, b.c1);
+#pragma unroll
+  for (int i = 0; i < 14; i++) nb1.l[i] = B[i] - b.c1.l[i];
   mul2(c0, a.c0, b.c0, a.c1, nb1);
   mul2(r.c1, a.c0, b.c1, a.c1, b.c0);
   r.c0 = c0;
@@ -228,6 +264,186 @@ HD void fe2_mul_xi(fe2 &r, const fe2 &a) {
   add(t1, a.c0, a.c1);
   r.c0 = t0;
   r.c1 = t1;
+}
+
+// ---------------------------------------------- sparse Miller-loop products (k_ml_group)
+// Every coefficient a routine returns is normalized and < 1.1 p ("S"); routines take S (or
+// normalized sums of two S) and follow the engine's formulas (bls_pairing.h sp_mul_sp,
+// fp6_mul_01, fp6_mul_1, fp12_mul_034), with each subtraction weakly reduced.
+struct fe6 {
+  fe2 c0, c1, c2;
+};
+struct fe12 {
+  fe6 c0, c1;
+};
+struct sp {  // a0 + a2 w^2 + a3 w^3
+  fe2 a0, a2, a3;
+};
+
+HD void fe2_add_lazy(fe2 &r, const fe2 &a, const fe2 &b) {
+  add_lazy(r.c0, a.c0, b.c0);
+  add_lazy(r.c1, a.c1, b.c1);
+}
+HD void fe2_sub_r(fe2 &r, const fe2 &a, const fe2 &b) {
+  sub_r(r.c0, a.c0, b.c0);
+  sub_r(r.c1, a.c1, b.c1);
+}
+// a + b, weakly reduced
+HD void fe2_add_r(fe2 &r, const fe2 &a, const fe2 &b) {
+  add(r.c0, a.c0, b.c0);
+  add(r.c1, a.c1, b.c1);
+  wred(r.c0);
+  wred(r.c1);
+}
+HD void fe2_zero(fe2 &r) {
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.c0.l[i] = r.c1.l[i] = 0;
+}
+// times xi = 1 + u
+HD void fe2_mul_xi_r(fe2 &r, const fe2 &a) {
+  fe t0, t1;
+  sub_r(t0, a.c0, a.c1);
+  add(t1, a.c0, a.c1);
+  wred(t1);
+  r.c0 = t0;
+  r.c1 = t1;
+}
+HD void fe6_add(fe6 &r, const fe6 &a, const fe6 &b) {  // normalized, not reduced
+  fe2_add_lazy(r.c0, a.c0, b.c0);
+  fe2_add_lazy(r.c1, a.c1, b.c1);
+  fe2_add_lazy(r.c2, a.c2, b.c2);
+  norm(r.c0.c0), norm(r.c0.c1), norm(r.c1.c0), norm(r.c1.c1), norm(r.c2.c0), norm(r.c2.c1);
+}
+HD void fe6_sub_r(fe6 &r, const fe6 &a, const fe6 &b) {
+  fe2_sub_r(r.c0, a.c0, b.c0);
+  fe2_sub_r(r.c1, a.c1, b.c1);
+  fe2_sub_r(r.c2, a.c2, b.c2);
+}
+
+// (a0 + a2 w^2 + a3 w^3)(b0 + b2 w^2 + b3 w^3): 6 Fp2 products
+HD void sp_mul_sp(fe12 &r, const sp &a, const sp &b) {
+  fe2 t0, t2, t3, sa, sb, u;
+  fe2_mul(t0, a.a0, b.a0);
+  fe2_mul(t2, a.a2, b.a2);
+  fe2_mul(t3, a.a3, b.a3);
+  fe2_mul_xi_r(u, t3);
+  fe2_add_r(r.c0.c0, t0, u);
+  fe2_zero(r.c1.c0);
+  fe2_add_lazy(sa, a.a0, a.a2);
+  fe2_add_lazy(sb, b.a0, b.a2);
+  norm(sb.c0), norm(sb.c1);
+  fe2_mul(u, sa, sb);
+  fe2_sub_r(u, u, t0);
+  fe2_sub_r(r.c0.c1, u, t2);
+  fe2_add_lazy(sa, a.a0, a.a3);
+  fe2_add_lazy(sb, b.a0, b.a3);
+  norm(sb.c0), norm(sb.c1);
+  fe2_mul(u, sa, sb);
+  fe2_sub_r(u, u, t0);
+  fe2_sub_r(r.c1.c1, u, t3);
+  r.c0.c2 = t2;
+  fe2_add_lazy(sa, a.a2, a.a3);
+  fe2_add_lazy(sb, b.a2, b.a3);
+  norm(sb.c0), norm(sb.c1);
+  fe2_mul(u, sa, sb);
+  fe2_sub_r(u, u, t2);
+  fe2_sub_r(r.c1.c2, u, t3);
+}
+// a (b0 + b1 v): 5 Fp2 products; a, b0, b1 normalized and < 2.2 p
+HD void fe6_mul_01(fe6 &r, const fe6 &a, const fe2 &b0, const fe2 &b1) {
+  fe2 t0, t1, s0, s1, c0, c1, c2;
+  fe2_mul(t0, a.c0, b0);
+  fe2_mul(t1, a.c1, b1);
+  fe2_add_lazy(s0, a.c1, a.c2);
+  fe2_mul(c0, s0, b1);
+  fe2_sub_r(c0, c0, t1);
+  fe2_mul_xi_r(c0, c0);
+  fe2_add_r(c0, c0, t0);
+  fe2_add_lazy(s0, a.c0, a.c1);
+  fe2_add_lazy(s1, b0, b1);
+  norm(s1.c0), norm(s1.c1);
+  fe2_mul(c1, s0, s1);
+  fe2_sub_r(c1, c1, t0);
+  fe2_sub_r(c1, c1, t1);
+  fe2_add_lazy(s0, a.c0, a.c2);
+  fe2_mul(c2, s0, b0);
+  fe2_sub_r(c2, c2, t0);
+  fe2_add_r(c2, c2, t1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+// a (b1 v): 3 Fp2 products
+HD void fe6_mul_1(fe6 &r, const fe6 &a, const fe2 &b1) {
+  fe2 c0, c1, c2;
+  fe2_mul(c0, a.c2, b1);
+  fe2_mul_xi_r(c0, c0);
+  fe2_mul(c1, a.c0, b1);
+  fe2_mul(c2, a.c1, b1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+// f (l0 + l2 w^2 + l3 w^3) = f ((l0 + l2 v) + (l3 v) w): 13 Fp2 products
+HD void fe12_mul_034(fe12 &r, const fe12 &a, const sp &s) {
+  fe6 t0, t1, u;
+  fe6_mul_01(t0, a.c0, s.a0, s.a2);
+  fe6_mul_1(t1, a.c1, s.a3);
+  fe6_add(u, a.c0, a.c1);
+  fe2 l23;
+  fe2_add_lazy(l23, s.a2, s.a3);
+  norm(l23.c0), norm(l23.c1);
+  fe6_mul_01(u, u, s.a0, l23);
+  fe6_sub_r(u, u, t0);
+  fe6_sub_r(r.c1, u, t1);
+  fe2 x;
+  fe2_mul_xi_r(x, t1.c2);  // t1 v
+  fe2_add_r(r.c0.c0, t0.c0, x);
+  fe2_add_r(r.c0.c1, t0.c1, t1.c0);
+  fe2_add_r(r.c0.c2, t0.c2, t1.c1);
+}
+// sparse line from engine-form line coefficients and an engine-form g1s point, with no
+// conversion: the product of two engine-form words over R = 2^392 is the radix-2^28 form of
+// L P times 2^-16, a scalar that the final exponentiation removes (as the g1s scaling does)
+HD void sp_from_engine(sp &s, const fp2 &L0, const fp2 &L2, const fp2 &L3, const fp &Px,
+                       const fp &Py, const fp &Pc) {
+  fe x, y, c, t0, t1;
+  repack_in(c, Pc);
+  repack_in(x, Px);
+  repack_in(y, Py);
+  repack_in(t0, L0.c0), repack_in(t1, L0.c1);
+  mul(s.a0.c0, t0, c), mul(s.a0.c1, t1, c);
+  repack_in(t0, L2.c0), repack_in(t1, L2.c1);
+  mul(s.a2.c0, t0, x), mul(s.a2.c1, t1, x);
+  repack_in(t0, L3.c0), repack_in(t1, L3.c1);
+  mul(s.a3.c0, t0, y), mul(s.a3.c1, t1, y);
+}
+HD void sp_identity(sp &s) {  // 2^-392 (raw limb 1): a nonzero scalar
+  fe2_zero(s.a0);
+  s.a0.c0.l[0] = 1;
+  fe2_zero(s.a2);
+  fe2_zero(s.a3);
+}
+HD void sp_to_fe12(fe12 &r, const sp &s) {
+  r.c0.c0 = s.a0;
+  r.c0.c1 = s.a2;
+  fe2_zero(r.c0.c2);
+  fe2_zero(r.c1.c0);
+  r.c1.c1 = s.a3;
+  fe2_zero(r.c1.c2);
+}
+// engine-form words of the value (canonical): f times 2^8 in the engine's reading
+HD void fe12_to_engine_scaled(fp12 &r, const fe12 &a) {
+  const fe *src[12] = {&a.c0.c0.c0, &a.c0.c0.c1, &a.c0.c1.c0, &a.c0.c1.c1, &a.c0.c2.c0, &a.c0.c2.c1,
+                       &a.c1.c0.c0, &a.c1.c0.c1, &a.c1.c1.c0, &a.c1.c1.c1, &a.c1.c2.c0, &a.c1.c2.c1};
+  fp *dst[12] = {&r.c0.c0.c0, &r.c0.c0.c1, &r.c0.c1.c0, &r.c0.c1.c1, &r.c0.c2.c0, &r.c0.c2.c1,
+                 &r.c1.c0.c0, &r.c1.c0.c1, &r.c1.c1.c0, &r.c1.c1.c1, &r.c1.c2.c0, &r.c1.c2.c1};
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    fe t = *src[i];
+    (void)sub_p_if_geq(t);  // < 1.1 p -> < p
+    repack_out(*dst[i], t);
+  }
 }
 
 }  // namespace r28

@@ -40,6 +40,7 @@ static_assert(sizeof(g2a) == sizeof(gbls_p2_affine), "p2 layout");
 static_assert(sizeof(fp12) == sizeof(gbls_fp12), "fp12 layout");
 
 uint32_t gbls::g_row_clear_max = gbls::kRowClearMax;
+uint32_t gbls::g_ml_r28 = 0;
 
 namespace {
 
@@ -350,6 +351,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
   if (const char *e = std::getenv("GBLS_SIDE2_HIGH")) g.side2_high = std::atoi(e) != 0;
   if (const char *e = std::getenv("GBLS_PRIO_MODE")) g.prio_mode = std::atoi(e);
   if (const char *e = std::getenv("GBLS_ROW_CLEAR_MAX")) g_row_clear_max = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
   for (int id : ids) {

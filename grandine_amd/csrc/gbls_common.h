@@ -25,6 +25,7 @@ constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
 constexpr uint32_t kRowRegimeMax = 6144;
 constexpr uint32_t kRowClearMax = 4096;  // cofactor clearing on rows (up to one C2 batch)
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
+extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic (GBLS_ML_R28)
 // line-coefficient buffer bound per submission (19.6 KB per pair: 4 GB = 214k pairs,
 // a C5 shard of 131 072 sets unsliced; tiny next to 288 GB of HBM): above it the Miller
 // lines are made in event slices (GBLS_LINE_BUDGET_MB overrides it)

@@ -9,6 +9,7 @@
 //   k_ml_reduce wave per (event, group of <= 4 values of one segment): wave-cooperative
 //               Fp12 products (bls_wave12.h)
 //   k_ml_horner wave per segment: Horner over the 68 events, then conj (x < 0)
+#include "bls_field28.h"
 #include "bls_wave12.h"
 #include "gbls_common.h"
 
@@ -45,6 +46,44 @@ __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np,
     }
   }
   V0[(size_t)e * ngroup + g] = acc;
+}
+
+// k_ml_group in radix-2^28 arithmetic (bls_field28.h; GBLS_ML_R28=1): same grid, same
+// inputs, and an output that differs from k_ml_group's by an Fp scalar (2^-16 per line and
+// 2^8 from the engine-form reading), which the final exponentiation removes
+__device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_t np, const g1s *P,
+                                          uint32_t pair, int e) {
+  fp2 L0, L2, L3;
+  line_get(L, np, pair, e, L0, L2, L3);
+  g1s Pp = P[pair];
+  if (fp_is_zero(Pp.c))
+    r28::sp_identity(s);
+  else
+    r28::sp_from_engine(s, L0, L2, L3, Pp.x, Pp.y, Pp.c);
+}
+__global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t np, const g1s *P,
+                                                   const uint32_t *plist, const uint32_t *grp,
+                                                   uint32_t ngroup, int e0, fp12 *V0) {
+  uint32_t g = blockIdx.x * WG + threadIdx.x;
+  int el = blockIdx.y, e = e0 + el;
+  if (g >= ngroup) return;
+  uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
+  r28::sp sa, sb;
+  r28::fe12 acc;
+  ml_eval28(sa, L, np, P, plist[at], el);
+  if (cnt == 1) {
+    r28::sp_to_fe12(acc, sa);
+  } else {
+    ml_eval28(sb, L, np, P, plist[at + stride], el);
+    r28::sp_mul_sp(acc, sa, sb);
+    for (uint32_t j = 2; j < cnt; j++) {
+      ml_eval28(sa, L, np, P, plist[at + j * stride], el);
+      r28::fe12_mul_034(acc, acc, sa);
+    }
+  }
+  fp12 out;
+  r28::fe12_to_engine_scaled(out, acc);
+  V0[(size_t)e * ngroup + g] = out;
 }
 
 // copy one Fp12 image global <-> LDS with all 64 lanes
@@ -96,7 +135,11 @@ void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g
                      const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
                      int e1, fp12 *V0) {
   dim3 grid(nblk(ngroup), e1 - e0);
-  if (ngroup && e1 > e0) k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
+  if (!ngroup || e1 <= e0) return;
+  if (g_ml_r28)
+    k_ml_group28<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
+  else
+    k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
 }
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout) {

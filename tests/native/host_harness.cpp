@@ -65,6 +65,90 @@ int h_r28_op(int op, const uint32_t *a, const uint32_t *b, const uint32_t *c, co
   return ret;
 }
 
+// radix-2^28 sparse Miller products (bls_field28.h) against the engine's (bls_pairing.h) on
+// random operands: sp x sp, then a chain of dense x sparse products; and the uniform scalar
+// of sp_from_engine.  Returns the number of mismatching Fp coefficients.
+static uint64_t h_rng = 1;
+static void h_rand_fp(fp &a) {
+  for (int i = 0; i < 12; i++) {
+    h_rng = h_rng * 6364136223846793005ull + 1442695040888963407ull;
+    a.l[i] = (uint32_t)(h_rng >> 32);
+  }
+  a.l[11] &= 0x0fffffff;  // < 2^380 < p
+}
+static void h_rand_fp2(fp2 &a) {
+  h_rand_fp(a.c0);
+  h_rand_fp(a.c1);
+}
+static int h_fp_differs(const fp &x, const fp &y) {
+  fp d;
+  fp_sub(d, x, y);
+  return !fp_is_zero(d);
+}
+static void h_to28(r28::fe2 &r, const fp2 &a) {
+  r28::from_fp(r.c0, a.c0);
+  r28::from_fp(r.c1, a.c1);
+}
+static int h_cmp12(const fp12 &e, const r28::fe12 &q) {
+  const fp *ev[12] = {&e.c0.c0.c0, &e.c0.c0.c1, &e.c0.c1.c0, &e.c0.c1.c1, &e.c0.c2.c0, &e.c0.c2.c1,
+                      &e.c1.c0.c0, &e.c1.c0.c1, &e.c1.c1.c0, &e.c1.c1.c1, &e.c1.c2.c0, &e.c1.c2.c1};
+  const r28::fe *qv[12] = {&q.c0.c0.c0, &q.c0.c0.c1, &q.c0.c1.c0, &q.c0.c1.c1, &q.c0.c2.c0,
+                           &q.c0.c2.c1, &q.c1.c0.c0, &q.c1.c0.c1, &q.c1.c1.c0, &q.c1.c1.c1,
+                           &q.c1.c2.c0, &q.c1.c2.c1};
+  int bad = 0;
+  for (int i = 0; i < 12; i++) {
+    fp t;
+    r28::to_fp(t, *qv[i]);
+    bad += h_fp_differs(t, *ev[i]);
+  }
+  return bad;
+}
+int h_r28_tower_check(uint64_t seed, int rounds, int chain) {
+  h_rng = seed;
+  int bad = 0;
+  for (int it = 0; it < rounds; it++) {
+    sp034 ea, eb;
+    r28::sp qa, qb;
+    h_rand_fp2(ea.a0), h_rand_fp2(ea.a2), h_rand_fp2(ea.a3);
+    h_rand_fp2(eb.a0), h_rand_fp2(eb.a2), h_rand_fp2(eb.a3);
+    h_to28(qa.a0, ea.a0), h_to28(qa.a2, ea.a2), h_to28(qa.a3, ea.a3);
+    h_to28(qb.a0, eb.a0), h_to28(qb.a2, eb.a2), h_to28(qb.a3, eb.a3);
+    fp12 ef;
+    r28::fe12 qf;
+    sp_mul_sp(ef, ea, eb);
+    r28::sp_mul_sp(qf, qa, qb);
+    bad += h_cmp12(ef, qf);
+    for (int j = 0; j < chain; j++) {
+      h_rand_fp2(ea.a0), h_rand_fp2(ea.a2), h_rand_fp2(ea.a3);
+      h_to28(qa.a0, ea.a0), h_to28(qa.a2, ea.a2), h_to28(qa.a3, ea.a3);
+      fp12_mul_034(ef, ef, ea);
+      r28::fe12_mul_034(qf, qf, qa);
+    }
+    bad += h_cmp12(ef, qf);
+    // sp_from_engine: engine line at (x, y, c) up to one scalar for all six coefficients
+    fp2 L0, L2, L3;
+    g1s P;
+    h_rand_fp2(L0), h_rand_fp2(L2), h_rand_fp2(L3);
+    h_rand_fp(P.x), h_rand_fp(P.y), h_rand_fp(P.c);
+    sp034 es;
+    line_eval_s(es, L0, L2, L3, P);
+    r28::sp qs;
+    r28::sp_from_engine(qs, L0, L2, L3, P.x, P.y, P.c);
+    const fp *ev[6] = {&es.a0.c0, &es.a0.c1, &es.a2.c0, &es.a2.c1, &es.a3.c0, &es.a3.c1};
+    const r28::fe *qv[6] = {&qs.a0.c0, &qs.a0.c1, &qs.a2.c0, &qs.a2.c1, &qs.a3.c0, &qs.a3.c1};
+    fp q0;
+    r28::to_fp(q0, *qv[0]);
+    for (int i = 1; i < 6; i++) {  // q_i e_0 == q_0 e_i
+      fp qi, l, r;
+      r28::to_fp(qi, *qv[i]);
+      fp_mul(l, qi, *ev[0]);
+      fp_mul(r, q0, *ev[i]);
+      bad += h_fp_differs(l, r);
+    }
+  }
+  return bad;
+}
+
 int h_g1_decompress(const uint8_t *in, int validate, uint8_t *out96) {
   g1a a;
   int s = g1_decompress(a, in);

@@ -215,3 +215,11 @@ def test_radix28_field_layer(H):
         assert run(6)[0] == (a == b)
     r, r2 = ctypes.create_string_buffer(48), ctypes.create_string_buffer(48)
     assert H.h_r28_op(6, m(5), m(5), m(0), m(0), r, r2) == 1
+
+
+def test_radix28_sparse_miller_products(H):
+    """bls_field28.h's sparse Miller products (the r28 k_ml_group path) equal the engine's
+    (bls_pairing.h) on random operands, through 40-step dense x sparse chains; sp_from_engine
+    differs from line_eval_s by one scalar shared by all coefficients."""
+    H.h_r28_tower_check.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+    assert H.h_r28_tower_check(7, 30, 40) == 0
