@@ -402,6 +402,41 @@ HD void fe12_mul_034(fe12 &r, const fe12 &a, const sp &s) {
   fe2_add_r(r.c0.c1, t0.c1, t1.c0);
   fe2_add_r(r.c0.c2, t0.c2, t1.c1);
 }
+// fe12_mul_034 with t1 = a.c1 s.a3 parked in a per-lane stash (LDS in k_ml_group28, word i of
+// the lane at st[i * stride]) while the Karatsuba middle product runs: 84 fewer live registers
+HD void fe6_stash(uint32_t *st, uint32_t stride, const fe6 &a) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(&a);
+#pragma unroll
+  for (int i = 0; i < 84; i++) st[i * stride] = w[i];
+}
+HD void fe6_unstash(fe6 &a, const uint32_t *st, uint32_t stride) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(&a);
+#pragma unroll
+  for (int i = 0; i < 84; i++) w[i] = st[i * stride];
+}
+HD void fe12_mul_034_st(fe12 &r, const fe12 &a, const sp &s, uint32_t *st, uint32_t stride) {
+  {
+    fe6 t1;
+    fe6_mul_1(t1, a.c1, s.a3);
+    fe6_stash(st, stride, t1);
+  }
+  fe6 t0, u;
+  fe6_mul_01(t0, a.c0, s.a0, s.a2);
+  fe6_add(u, a.c0, a.c1);
+  fe2 l23;
+  fe2_add_lazy(l23, s.a2, s.a3);
+  norm(l23.c0), norm(l23.c1);
+  fe6_mul_01(u, u, s.a0, l23);
+  fe6_sub_r(u, u, t0);
+  fe6 t1;
+  fe6_unstash(t1, st, stride);
+  fe6_sub_r(r.c1, u, t1);
+  fe2 x;
+  fe2_mul_xi_r(x, t1.c2);
+  fe2_add_r(r.c0.c0, t0.c0, x);
+  fe2_add_r(r.c0.c1, t0.c1, t1.c0);
+  fe2_add_r(r.c0.c2, t0.c2, t1.c1);
+}
 // sparse line from engine-form line coefficients and an engine-form g1s point, with no
 // conversion: the product of two engine-form words over R = 2^392 is the radix-2^28 form of
 // L P times 2^-16, a scalar that the final exponentiation removes (as the g1s scaling does)

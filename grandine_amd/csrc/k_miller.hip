@@ -68,6 +68,7 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
   int el = blockIdx.y, e = e0 + el;
   if (g >= ngroup) return;
   uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
+  __shared__ uint32_t stash[84 * WG];
   r28::sp sa, sb;
   r28::fe12 acc;
   ml_eval28(sa, L, np, P, plist[at], el);
@@ -78,7 +79,7 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
     r28::sp_mul_sp(acc, sa, sb);
     for (uint32_t j = 2; j < cnt; j++) {
       ml_eval28(sa, L, np, P, plist[at + j * stride], el);
-      r28::fe12_mul_034(acc, acc, sa);
+      r28::fe12_mul_034_st(acc, acc, sa, stash + threadIdx.x, WG);
     }
   }
   fp12 out;

@@ -122,7 +122,12 @@ int h_r28_tower_check(uint64_t seed, int rounds, int chain) {
       h_rand_fp2(ea.a0), h_rand_fp2(ea.a2), h_rand_fp2(ea.a3);
       h_to28(qa.a0, ea.a0), h_to28(qa.a2, ea.a2), h_to28(qa.a3, ea.a3);
       fp12_mul_034(ef, ef, ea);
-      r28::fe12_mul_034(qf, qf, qa);
+      if (j & 1) {
+        uint32_t st[84 * 3];
+        r28::fe12_mul_034_st(qf, qf, qa, st + 1, 3);
+      } else {
+        r28::fe12_mul_034(qf, qf, qa);
+      }
     }
     bad += h_cmp12(ef, qf);
     // sp_from_engine: engine line at (x, y, c) up to one scalar for all six coefficients
