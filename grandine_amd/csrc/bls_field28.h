@@ -83,24 +83,29 @@ HD void mul_n(fe &r, const fe *const *x, const fe *const *y) {
     acc >>= 28;
   }
   t[13] = (uint32_t)acc;
-#if defined(__HIP_DEVICE_COMPILE__)
-  // a scheduling boundary after every product: the compiler keeps products in source order
-  // instead of interleaving independent ones (which spills; see tools/gen_fpmul.py)
-  asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]),
-               "+v"(t[6]), "+v"(t[7]), "+v"(t[8]), "+v"(t[9]), "+v"(t[10]), "+v"(t[11]),
-               "+v"(t[12]), "+v"(t[13]));
-#endif
 #pragma unroll
   for (int i = 0; i < 14; i++) r.l[i] = t[i];
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+constexpr uint32_t kP28[14] = {GBLS_R28_P};
+#include "bls_fpmul28_gen.h"
+#endif
 HD void mul(fe &r, const fe &a, const fe &b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mul_dev(r, a, b);
+#else
   const fe *x[1] = {&a}, *y[1] = {&b};
   mul_n<1>(r, x, y);
+#endif
 }
 // a b + c d in one reduction
 HD void mul2(fe &r, const fe &a, const fe &b, const fe &c, const fe &d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mul2_dev(r, a, b, c, d);
+#else
   const fe *x[2] = {&a, &c}, *y[2] = {&b, &d};
   mul_n<2>(r, x, y);
+#endif
 }
 
 HD void norm(fe &a) {
@@ -414,6 +419,8 @@ HD void fe6_unstash(fe6 &a, const uint32_t *st, uint32_t stride) {
 #pragma unroll
   for (int i = 0; i < 84; i++) w[i] = st[i * stride];
 }
+// and the first 70 words of t0 at st[(84 + i) * stride] during it (154 words: 4 waves of 64
+// lanes per CU stay within 160 KB of LDS)
 HD void fe12_mul_034_st(fe12 &r, const fe12 &a, const sp &s, uint32_t *st, uint32_t stride) {
   {
     fe6 t1;
@@ -423,10 +430,20 @@ HD void fe12_mul_034_st(fe12 &r, const fe12 &a, const sp &s, uint32_t *st, uint3
   fe6 t0, u;
   fe6_mul_01(t0, a.c0, s.a0, s.a2);
   fe6_add(u, a.c0, a.c1);
+  {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&t0);
+#pragma unroll
+    for (int i = 0; i < 70; i++) st[(84 + i) * stride] = w[i];
+  }
   fe2 l23;
   fe2_add_lazy(l23, s.a2, s.a3);
   norm(l23.c0), norm(l23.c1);
   fe6_mul_01(u, u, s.a0, l23);
+  {
+    uint32_t *w = reinterpret_cast<uint32_t *>(&t0);
+#pragma unroll
+    for (int i = 0; i < 70; i++) w[i] = st[(84 + i) * stride];
+  }
   fe6_sub_r(u, u, t0);
   fe6 t1;
   fe6_unstash(t1, st, stride);
@@ -442,16 +459,16 @@ HD void fe12_mul_034_st(fe12 &r, const fe12 &a, const sp &s, uint32_t *st, uint3
 // L P times 2^-16, a scalar that the final exponentiation removes (as the g1s scaling does)
 HD void sp_from_engine(sp &s, const fp2 &L0, const fp2 &L2, const fp2 &L3, const fp &Px,
                        const fp &Py, const fp &Pc) {
-  fe x, y, c, t0, t1;
-  repack_in(c, Pc);
-  repack_in(x, Px);
-  repack_in(y, Py);
-  repack_in(t0, L0.c0), repack_in(t1, L0.c1);
-  mul(s.a0.c0, t0, c), mul(s.a0.c1, t1, c);
-  repack_in(t0, L2.c0), repack_in(t1, L2.c1);
-  mul(s.a2.c0, t0, x), mul(s.a2.c1, t1, x);
-  repack_in(t0, L3.c0), repack_in(t1, L3.c1);
-  mul(s.a3.c0, t0, y), mul(s.a3.c1, t1, y);
+  fe q, t;
+  repack_in(q, Pc);
+  repack_in(t, L0.c0), mul(s.a0.c0, t, q);
+  repack_in(t, L0.c1), mul(s.a0.c1, t, q);
+  repack_in(q, Px);
+  repack_in(t, L2.c0), mul(s.a2.c0, t, q);
+  repack_in(t, L2.c1), mul(s.a2.c1, t, q);
+  repack_in(q, Py);
+  repack_in(t, L3.c0), mul(s.a3.c0, t, q);
+  repack_in(t, L3.c1), mul(s.a3.c1, t, q);
 }
 HD void sp_identity(sp &s) {  // 2^-392 (raw limb 1): a nonzero scalar
   fe2_zero(s.a0);

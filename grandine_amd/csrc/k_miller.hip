@@ -55,7 +55,7 @@ __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_
                                           uint32_t pair, int e) {
   fp2 L0, L2, L3;
   line_get(L, np, pair, e, L0, L2, L3);
-  g1s Pp = P[pair];
+  const g1s &Pp = P[pair];
   if (fp_is_zero(Pp.c))
     r28::sp_identity(s);
   else
@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
   int el = blockIdx.y, e = e0 + el;
   if (g >= ngroup) return;
   uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
-  __shared__ uint32_t stash[84 * WG];
+  __shared__ uint32_t stash[154 * WG];
   r28::sp sa, sb;
   r28::fe12 acc;
   ml_eval28(sa, L, np, P, plist[at], el);

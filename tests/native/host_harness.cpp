@@ -123,7 +123,7 @@ int h_r28_tower_check(uint64_t seed, int rounds, int chain) {
       h_to28(qa.a0, ea.a0), h_to28(qa.a2, ea.a2), h_to28(qa.a3, ea.a3);
       fp12_mul_034(ef, ef, ea);
       if (j & 1) {
-        uint32_t st[84 * 3];
+        uint32_t st[154 * 3];
         r28::fe12_mul_034_st(qf, qf, qa, st + 1, 3);
       } else {
         r28::fe12_mul_034(qf, qf, qa);
