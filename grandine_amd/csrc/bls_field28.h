@@ -17,8 +17,9 @@
 //   neg_lazy(a) = 4p - a needs a < 2p.
 // canon() gives the unique representative in [0, p) (values < 16 p).
 #pragma once
-
-#include "bls_field.h"
+// needs bls_field.h (struct fp, HD) included first; bls_field.h itself includes this header
+// under GBLS_POW_R28
+#include <stdint.h>
 
 namespace gbls {
 namespace r28 {

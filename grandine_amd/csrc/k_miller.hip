@@ -9,8 +9,8 @@
 //   k_ml_reduce wave per (event, group of <= 4 values of one segment): wave-cooperative
 //               Fp12 products (bls_wave12.h)
 //   k_ml_horner wave per segment: Horner over the 68 events, then conj (x < 0)
-#include "bls_field28.h"
 #include "bls_wave12.h"
+#include "bls_field28.h"
 #include "gbls_common.h"
 
 namespace gbls {

@@ -24,8 +24,11 @@ def gold(name):
 def H():
     src = os.path.join(ROOT, "tests", "native", "host_harness.cpp")
     os.makedirs(os.path.dirname(SO), exist_ok=True)
+    # GBLS_HARNESS_DEFS: extra -D flags, to check an experiment build's arithmetic (e.g.
+    # -DGBLS_POW_R28) with the same tests
+    defs = os.environ.get("GBLS_HARNESS_DEFS", "").split()
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-D__HIP_PLATFORM_AMD__",
-                           "-I/opt/rocm/include", "-o", SO, src])
+                           "-I/opt/rocm/include"] + defs + ["-o", SO, src])
     L = ctypes.CDLL(SO)
     L.h_multi_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "../../grandine_amd/csrc/bls_field.h"
 #include "../../grandine_amd/csrc/bls_field28.h"
 
 // the layer under test: grandine_amd/csrc/bls_field28.h (mul28<NACC> below is the
