@@ -1,6 +1,7 @@
-// Radix-2^28 arithmetic over the BLS12-381 base field: the next field layer, not yet used by the
-// kernels (tools/ubench/r28_bench.hip measured its product at 1.40x the
-// engine's product per lane on MI355X).
+// Radix-2^28 arithmetic over the BLS12-381 base field: the next field layer,
+// used so far by the (p-3)/4 exponentiation (hash_to_G2's SSWU, decompression square roots)
+// and the GBLS_ML_R28 k_ml_group28; tools/ubench/r28_bench.hip measured its product at 1.40x
+// the engine's product per lane on MI355X.
 //
 // An element is 14 limbs of 28 bits in Montgomery form with R = 2^392.  A column of the
 // product-scanning Montgomery product holds at most 28 terms (42 for a dual product), so with
@@ -18,7 +19,7 @@
 // canon() gives the unique representative in [0, p) (values < 16 p).
 #pragma once
 // needs bls_field.h (struct fp, HD) included first; bls_field.h itself includes this header
-// under GBLS_POW_R28
+// for its (p-3)/4 exponentiation (unless GBLS_POW_ENGINE)
 #include <stdint.h>
 
 namespace gbls {

@@ -25,7 +25,7 @@ def H():
     src = os.path.join(ROOT, "tests", "native", "host_harness.cpp")
     os.makedirs(os.path.dirname(SO), exist_ok=True)
     # GBLS_HARNESS_DEFS: extra -D flags, to check an experiment build's arithmetic (e.g.
-    # -DGBLS_POW_R28) with the same tests
+    # -DGBLS_POW_ENGINE) with the same tests
     defs = os.environ.get("GBLS_HARNESS_DEFS", "").split()
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-D__HIP_PLATFORM_AMD__",
                            "-I/opt/rocm/include"] + defs + ["-o", SO, src])
