@@ -156,6 +156,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's host CPU share")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tuning", action="store_true",
+                    help="let the engine read its GBLS_* tuning environment variables (sweeps)")
     args = ap.parse_args()
 
     import numpy as np
@@ -182,6 +184,8 @@ def main():
     from grandine_amd import _lib as G
     from grandine_amd import factory as F
 
+    if args.tuning:
+        G.enable_tuning()
     L = G.lib(1 << dev.index, 0)
 
     def dbytes(b):

@@ -11,9 +11,31 @@ import ctypes
 import os
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgrandine_bls.so")
-# experiment builds (tools/): another in-tree build of the same library
-LIB_PATH = os.environ.get("GBLS_LIB", LIB_PATH)
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libgrandine_bls.so")
+# Experiment builds (tools/gpu sweeps): GBLS_LIB may name another build of the library
+# INSIDE this package directory (make LIB=lib_x ...); anything else is refused, so a stray
+# environment variable cannot swap the verifier for an arbitrary shared object.
+_override = os.environ.get("GBLS_LIB")
+if _override:
+    _real = os.path.realpath(_override)
+    if os.path.commonpath([_real, os.path.realpath(_PKG)]) != os.path.realpath(_PKG):
+        raise ImportError(f"GBLS_LIB={_override!r} is outside {_PKG}; refusing to load it")
+    import sys as _sys
+
+    print(f"grandine_amd: experiment build {_real} (GBLS_LIB)", file=_sys.stderr)
+    LIB_PATH = _real
+
+# GBLS_INIT_TUNING (include/grandine_bls_gpu.h): tests and sweeps that set the engine's
+# tuning environment variables call enable_tuning() before the first lib() call.
+INIT_TUNING = 0x200
+_tuning = False
+
+
+def enable_tuning():
+    """Let the engine read its tuning environment variables (tests / sweeps only)."""
+    global _tuning
+    _tuning = True
 
 # status codes (BLST_ERROR mirror)
 SUCCESS = 0
@@ -171,6 +193,8 @@ def lib(device_mask: int = 0, flags: int = 0):
     if not _ready:
         with _lock:
             if not _ready:
+                if _tuning:
+                    flags |= INIT_TUNING
                 if L.gbls_init(device_mask, flags) != SUCCESS:
                     raise EngineUnavailable(
                         f"gbls_init failed (error {L.gbls_last_error()}): no usable gfx950 device")

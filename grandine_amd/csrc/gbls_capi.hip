@@ -343,15 +343,23 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
   }
   if (ids.empty()) return fail(GBLS_ERR_NO_DEVICE);
   g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
-  if (const char *e = std::getenv("GBLS_MSM_MIN")) g.msm_min = std::strtoull(e, nullptr, 10);
-  if (const char *e = std::getenv("GBLS_LINE_BUDGET_MB"))
-    g.line_budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
-  if (const char *e = std::getenv("GBLS_ML_G")) g.ml_g = (uint32_t)std::strtoul(e, nullptr, 10);
-  if (const char *e = std::getenv("GBLS_ML_ROUNDS")) g.ml_rounds = (uint32_t)std::strtoul(e, nullptr, 10);
-  if (const char *e = std::getenv("GBLS_SIDE2_HIGH")) g.side2_high = std::atoi(e) != 0;
-  if (const char *e = std::getenv("GBLS_PRIO_MODE")) g.prio_mode = std::atoi(e);
-  if (const char *e = std::getenv("GBLS_ROW_CLEAR_MAX")) g_row_clear_max = (uint32_t)std::strtoul(e, nullptr, 10);
-  if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
+  // tuning knobs: only for tests and sweeps that ask for them (GBLS_INIT_TUNING); a node
+  // embedding the library runs the measured defaults whatever its environment holds
+  if (flags & GBLS_INIT_TUNING) {
+    if (const char *e = std::getenv("GBLS_MSM_MIN")) g.msm_min = std::strtoull(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_LINE_BUDGET_MB"))
+      g.line_budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
+    if (const char *e = std::getenv("GBLS_ML_G")) g.ml_g = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_ML_ROUNDS"))
+      g.ml_rounds = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_SIDE2_HIGH")) g.side2_high = std::atoi(e) != 0;
+    if (const char *e = std::getenv("GBLS_PRIO_MODE")) g.prio_mode = std::atoi(e);
+    if (const char *e = std::getenv("GBLS_ROW_CLEAR_MAX"))
+      g_row_clear_max = (uint32_t)std::strtoul(e, nullptr, 10);
+#ifdef GBLS_EXPERIMENTS
+    if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
+#endif
+  }
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
   for (int id : ids) {
@@ -906,7 +914,6 @@ void run_merged(std::vector<CoReq *> &batch) {
     r.ok = verify_host(r.msgs, r.sigs, r.sigs_c, r.sig_status, r.src, r.rands, r.n, r.seg_off,
                        r.nseg, r.verdicts);
     r.err = t_last_error;
-    r.done = true;
     return;
   }
   size_t n = 0, nseg = 0, nk = 0;
@@ -962,7 +969,6 @@ void run_merged(std::vector<CoReq *> &batch) {
     at += r->n;
     r->ok = ok;
     r->err = err;
-    r->done = true;
   }
 }
 
@@ -997,8 +1003,9 @@ bool coalesced_verify(CoReq &r) {
         }
       }
       lk.unlock();
-      run_merged(batch);
+      run_merged(batch);  // writes verdicts, ok, err; `done` is published under co.mu
       lk.lock();
+      for (CoReq *b : batch) b->done = true;
       co.leaders--;
       co.cv.notify_all();
     } else {
@@ -1547,13 +1554,24 @@ int gbls_fast_aggregate_verify_indexed_device(const gbls_p2_affine *sigs, const 
              : FAILED;
 }
 
-// ---- validator registry (f1): bulk decompress + validate on the device, replicated
+// ---- validator registry (f1): bulk decompress + validate on the device, replicated.
+// The keys are decompressed ONCE (on the first engine device) and the 96-B affine table
+// slice is copied device-to-device to every other replica (hipMemcpyPeerAsync over xGMI
+// between GPUs), so 8 GPUs cost one decompression of the registry, not eight.  The new
+// size is committed only when every replica holds the slice; a failure part-way truncates
+// the registry to `first`, so no index can resolve to replicas that disagree (indices past
+// the size are BAD_ENCODING everywhere).
 int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t *status) {
   fill(status, n, GBLS_BAD_ENCODING);
   API_BEGIN
   std::unique_lock<std::shared_mutex> wl(g.reg_mu);
   size_t new_n = std::max(g.reg_n, first + n);
   if (new_n > 0xffffffffull) return fail(GBLS_ERR_ARG), FAILED;
+  auto broken = [&]() {
+    g.reg_n = std::min(g.reg_n, first);
+    fill(status, n, GBLS_BAD_ENCODING);
+    return FAILED;
+  };
   for (size_t j = 0; j < g.devs.size(); j++) {
     Device &d = *g.devs[j];
     if (hipSetDevice(d.hipdev) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
@@ -1571,20 +1589,27 @@ int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t 
   }
   if (n) {
     std::vector<int32_t> st0(n);
-    for (size_t j = 0; j < g.devs.size(); j++) {
+    Device &d0 = *g.devs[0];
+    Lease L(d0);
+    Ctx &c = *L;
+    hipStream_t st = c.own;
+    if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &pks[0][0], 48 * n, st) ||
+        !c.ensure(c.out1, n * sizeof(int32_t)))
+      return broken();
+    g1a *slice0 = d0.reg.as<g1a>() + first;
+    launch_g1_decompress(st, c.in0.as<uint8_t>(), (uint32_t)n, 1, slice0, c.out1.as<int32_t>());
+    if (hipMemcpyAsync(st0.data(), c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+      return fail(GBLS_ERR_HIP), broken();
+    // broadcast the decoded slice: queued on the same stream behind the decompression
+    for (size_t j = 1; j < g.devs.size(); j++) {
       Device &d = *g.devs[j];
-      Lease L(d);
-      Ctx &c = *L;
-      hipStream_t st = c.own;
-      if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &pks[0][0], 48 * n, st) ||
-          !c.ensure(c.out1, n * sizeof(int32_t)))
-        return FAILED;
-      launch_g1_decompress(st, c.in0.as<uint8_t>(), (uint32_t)n, 1, d.reg.as<g1a>() + first,
-                           c.out1.as<int32_t>());
-      if (hipMemcpyAsync(st0.data(), c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipStreamSynchronize(st) != hipSuccess)
-        return fail(GBLS_ERR_HIP), FAILED;
+      g1a *dst = d.reg.as<g1a>() + first;
+      hipError_t e = d.hipdev == d0.hipdev
+                         ? hipMemcpyAsync(dst, slice0, n * sizeof(g1a), hipMemcpyDeviceToDevice, st)
+                         : hipMemcpyPeerAsync(dst, d.hipdev, slice0, d0.hipdev, n * sizeof(g1a), st);
+      if (e != hipSuccess) return fail(GBLS_ERR_HIP), broken();
     }
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(GBLS_ERR_HIP), broken();
     std::memcpy(status, st0.data(), n * 4);
   }
   g.reg_n = new_n;

@@ -57,13 +57,17 @@ __global__ void __launch_bounds__(WGR) k_g2_aggregate_seg(const g2a *pts, const 
 // ---------------------------------------------------------------- validator registry (f1)
 // Public keys addressed by validator index into a device-resident table of decompressed,
 // validated keys (the CachedPublicKey cache, bls/src/cached_public_key.rs:104-108, one
-// per Validator.pubkey, types/src/phase0/containers.rs:229).  Invalid or out-of-range
-// entries are all-zero (infinity), which every verification path rejects.
+// per Validator.pubkey, types/src/phase0/containers.rs:229).  Invalid keys and slots never
+// loaded are stored all-zero (infinity).  A valid key is never infinity (PublicKey::try_from
+// validates, bls/src/public_key.rs:20-28), so every gather below flags an all-zero entry
+// BAD_ENCODING like an out-of-range index: the reference fails the whole check when one
+// member key does not decompress (helper_functions/src/predicates.rs:130).
 
 // one workgroup per segment: sum of reg[idx[off[s] .. off[s+1])] (Triple::verify_aggregate,
 // helper_functions/src/verifier.rs:387-405); st = AGGR_TYPE_MISMATCH when empty,
-// BAD_ENCODING when an index is out of range.  An infinite sum is a SUCCESS (as in
-// AggregatePublicKey::aggregate); the verification paths reject infinite keys.
+// BAD_ENCODING when an index is out of range or names an invalid / unloaded (all-zero)
+// entry.  An infinite sum of valid keys is a SUCCESS (as in AggregatePublicKey::aggregate);
+// the verification paths reject infinite keys.
 __global__ void __launch_bounds__(WGR) k_g1_aggregate_idx(const g1a *reg, uint32_t nreg,
                                                           const uint32_t *idx, const uint32_t *off,
                                                           uint32_t nseg, g1a *out, int32_t *st) {
@@ -78,7 +82,7 @@ __global__ void __launch_bounds__(WGR) k_g1_aggregate_idx(const g1a *reg, uint32
   int32_t oob = 0;
   for (uint32_t i = b + threadIdx.x; i < e; i += WGR) {
     uint32_t v = idx[i];
-    if (v < nreg)
+    if (v < nreg && !aff_is_inf(reg[v]))
       jac_add_aff(acc, acc, reg[v]);
     else
       oob = 1;
@@ -102,7 +106,8 @@ __global__ void __launch_bounds__(WGR) k_g1_aggregate_idx(const g1a *reg, uint32
   }
 }
 
-// one key per set: out[i] = reg[idx[i]] (all-zero + BAD_ENCODING when out of range)
+// one key per set: out[i] = reg[idx[i]] (all-zero + BAD_ENCODING when out of range or
+// the entry is invalid / unloaded)
 __global__ void __launch_bounds__(WG) k_g1_gather_idx(const g1a *reg, uint32_t nreg,
                                                       const uint32_t *idx, uint32_t n, g1a *out,
                                                       int32_t *st) {
@@ -110,14 +115,16 @@ __global__ void __launch_bounds__(WG) k_g1_gather_idx(const g1a *reg, uint32_t n
   if (i >= n) return;
   uint32_t v = idx[i];
   g1a r;
-  if (v < nreg) {
+  bool ok = v < nreg;
+  if (ok) {
     r = reg[v];
+    ok = !aff_is_inf(r);
   } else {
     fp_zero(r.x);
     fp_zero(r.y);
   }
   out[i] = r;
-  st[i] = v < nreg ? ST_SUCCESS : ST_BAD_ENCODING;
+  st[i] = ok ? ST_SUCCESS : ST_BAD_ENCODING;
 }
 
 // ---------------------------------------------------------------- row aggregation
@@ -155,7 +162,7 @@ __global__ void __launch_bounds__(WG) k_aggregate_rows(const aff<F> *pts, uint32
   uint32_t oob = 0;
   for (uint32_t i = b + r; i < e; i += 16) {
     uint32_t v = idx ? idx[i] : i;
-    if (idx && v >= nreg)
+    if (idx && (v >= nreg || aff_is_inf(pts[v])))  // registry: out of range / invalid slot
       oob = 1;
     else
       jac_add_aff(acc, acc, pts[v]);

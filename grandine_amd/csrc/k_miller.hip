@@ -48,6 +48,7 @@ __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np,
   V0[(size_t)e * ngroup + g] = acc;
 }
 
+#ifdef GBLS_EXPERIMENTS  // measured slower; not in the shipped build
 // k_ml_group in radix-2^28 arithmetic (bls_field28.h; GBLS_ML_R28=1): same grid, same
 // inputs, and an output that differs from k_ml_group's by an Fp scalar (2^-16 per line and
 // 2^8 from the engine-form reading), which the final exponentiation removes
@@ -86,6 +87,8 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
   r28::fe12_to_engine_scaled(out, acc);
   V0[(size_t)e * ngroup + g] = out;
 }
+
+#endif  // GBLS_EXPERIMENTS
 
 // copy one Fp12 image global <-> LDS with all 64 lanes
 __device__ __forceinline__ void w12_load(uint32_t *dst, const fp12 *src) {
@@ -137,10 +140,13 @@ void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g
                      int e1, fp12 *V0) {
   dim3 grid(nblk(ngroup), e1 - e0);
   if (!ngroup || e1 <= e0) return;
-  if (g_ml_r28)
+#ifdef GBLS_EXPERIMENTS
+  if (g_ml_r28) {
     k_ml_group28<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
-  else
-    k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
+    return;
+  }
+#endif
+  k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
 }
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout) {

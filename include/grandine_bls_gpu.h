@@ -106,8 +106,13 @@ enum {
 };
 
 /* gbls_init flags: low byte = engines per device; GBLS_INIT_NO_COALESCE turns off the
- * cross-caller coalescing of concurrent host-pointer multi_verify calls (f3). */
+ * cross-caller coalescing of concurrent host-pointer multi_verify calls (f3).
+ * GBLS_INIT_TUNING (tests and benchmark sweeps only) lets gbls_init read the engine's
+ * tuning environment variables (GBLS_MSM_MIN, GBLS_LINE_BUDGET_MB, GBLS_ML_G,
+ * GBLS_ML_ROUNDS, GBLS_PRIO_MODE, GBLS_SIDE2_HIGH, GBLS_ROW_CLEAR_MAX); without it the
+ * measured defaults are fixed and no environment variable changes the engine. */
 #define GBLS_INIT_NO_COALESCE 0x100u
+#define GBLS_INIT_TUNING 0x200u
 int gbls_init(uint32_t device_mask, uint32_t flags);
 int gbls_last_error(void);
 const char *gbls_version(void);

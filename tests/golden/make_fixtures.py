@@ -259,6 +259,10 @@ def main():
     fcase(agg_sig, m, [], "no keys")
     fcase(None, m, [pks[0], O.g1_neg(pks[0])], "keys cancel to infinity")
     fcase(sigs[2], msgs[2], [pks[2]], "single key")
+    fcase(None, m, [pks[i] for i in committee], "infinite signature")
+    fcase(bad_sig, m, [pks[i] for i in committee], "signature not in G2")
+    fcase(agg_sig, m, [pks[i] for i in committee] + [None], "infinity member key (aggregation skips it)")
+    fcase(O.sign(sks[0], m), m, [pks[0], None], "infinity member key, single signer")
     out["fast_aggregate_verify"] = {"provenance": "oracle (Signature::fast_aggregate_verify, signature.rs:77-93)",
                                     "cases": fav}
 

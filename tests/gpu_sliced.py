@@ -14,6 +14,7 @@ sys.path.insert(0, ROOT)
 os.environ["GBLS_LINE_BUDGET_MB"] = "16"
 
 from grandine_amd import _lib as G  # noqa: E402
+G.enable_tuning()  # the engine reads the knob set above
 from grandine_amd import factory as F  # noqa: E402
 
 

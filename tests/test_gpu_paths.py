@@ -325,6 +325,52 @@ def test_registry_invalid_keys_and_growth(G, L, F, registry):
     assert L.gbls_multi_verify_indexed(msgs, sig, G.u32_array([0]), None, u64([5]), 1) == G.SUCCESS
 
 
+def test_registry_aggregates_with_gap_or_invalid_member_fail(G, L, F, registry):
+    """an aggregate over registry indices that names a gap slot or an
+    invalid key must fail, not verify as if the member were absent (the reference fails
+    the check when a member key does not decompress, helper_functions/src/predicates.rs:130).
+    Covers the aggregation entry, multi_verify_indexed with pk_off (workgroup and row
+    kernels: 1 and 200 segments), fast_aggregate_verify_indexed, and the fused finish."""
+    sks, comp = registry
+    base = N_REG + 10  # test_registry_invalid_keys_and_growth: base = invalid, base + 1 = infinity
+    F.load_registry(bytes(48), first=base)  # (idempotent when run alone: an invalid key at base)
+    gap, invalid = N_REG + 1, base
+    msgs = F.messages(1, b"gap-agg")
+    sig = F.sign([sks[0]], msgs)  # signed by member 0 alone
+    for other in (gap, invalid):
+        idx = G.u32_array([0, other])
+        off = G.u32_array([0, 2])
+        agg = ctypes.create_string_buffer(96)
+        st = G.i32_array(1)
+        G.check(L.gbls_g1_aggregate_indexed(idx, off, 1, agg, st), "aggregate_indexed")
+        assert st[0] == G.BAD_ENCODING, other
+        assert L.gbls_multi_verify_indexed(msgs, sig, idx, off, u64([7]), 1) == G.VERIFY_FAIL, other
+        v = G.i32_array(1)
+        G.check(L.gbls_fast_aggregate_verify_indexed(sig, msgs, G.u32_array([0, 32]), idx, off, 1, v), "fav")
+        assert v[0] == G.VERIFY_FAIL, other
+        comp_sig = ctypes.create_string_buffer(96)
+        G.check(L.gbls_g2_compress(sig, 1, comp_sig), "compress")
+        sst = G.i32_array(1)
+        assert L.gbls_multi_verify_compressed(msgs, comp_sig, None, idx, off, u64([7]), 1, sst) == G.VERIFY_FAIL
+    # the same member alone verifies (the failure above is the gap / invalid member)
+    assert L.gbls_multi_verify_indexed(msgs, sig, G.u32_array([0]), G.u32_array([0, 1]), u64([7]), 1) == G.SUCCESS
+    # row kernel (>= 128 segments): 200 two-member committees, one with a gap member
+    m = 200
+    ms = F.messages(m, b"gap-rows")
+    sums = [(sks[2 * i] + sks[2 * i + 1]) % F.R_ORDER for i in range(m)]
+    sigs = F.sign(sums, ms)
+    idx = list(range(2 * m))
+    idx[2 * 123 + 1] = gap
+    st = G.i32_array(m)
+    agg = ctypes.create_string_buffer(96 * m)
+    G.check(L.gbls_g1_aggregate_indexed(G.u32_array(idx), G.u32_array(range(0, 2 * m + 1, 2)), m, agg, st), "agg")
+    assert [i for i in range(m) if st[i] != 0] == [123]
+    v = G.i32_array(m)
+    G.check(L.gbls_fast_aggregate_verify_indexed(sigs, ms, G.u32_array(range(0, 32 * m + 1, 32)), G.u32_array(idx),
+                                                 G.u32_array(range(0, 2 * m + 1, 2)), m, v), "fav rows")
+    assert [i for i in range(m) if v[i] != 0] == [123]
+
+
 def test_c4_epoch_aggregation_and_verify(G, L, F, REF, registry):
     """C4: 32 x 64 committees over a 2^20-key registry (sizes 511/512)."""
     sks, comp = registry
@@ -380,6 +426,35 @@ def test_c5_shard_indexed_131072(G, L, F, REF, registry):
     assert REF.ref_multi_verify(msgs[:32 * 2048], sigs[:192 * 2048], pk_pts, u64(rands[:2048]), 2048, 16) == 1
     assert L.gbls_multi_verify_indexed(msgs[:32 * 2048], sigs[:192 * 2048], idx_c, None, u64(rands[:2048]),
                                        2048) == G.SUCCESS
+
+
+def test_c5_full_2pow20_sliced_accept_and_reject(G, L, F, REF, registry):
+    """C5 at full size on one GPU: 2^20 sets from the 1.7M registry, whose Miller lines
+    exceed the 4 GB line budget and run in event slices.  Accepts the valid batch and
+    rejects one flipped message and, separately, one swapped signature pair near the end;
+    the C oracle agrees on a 2048-set slice around each corruption."""
+    sks, comp = registry
+    n = 1 << 20
+    rng = np.random.default_rng(20)
+    idx = rng.integers(0, N_REG, size=n, dtype=np.uint32)
+    msgs = F.messages(n, b"c5-full")
+    sigs = F.sign([sks[int(i)] for i in idx], msgs)
+    rands = F.rands(n, 20)
+    idx_c = idx.ctypes.data_as(ctypes.c_void_p)
+    assert L.gbls_multi_verify_indexed(msgs, sigs, idx_c, None, u64(rands), n) == G.SUCCESS
+    bad_m = bytearray(msgs)
+    bad_m[32 * 700001 + 3] ^= 0x01
+    bad_m = bytes(bad_m)
+    assert L.gbls_multi_verify_indexed(bad_m, sigs, idx_c, None, u64(rands), n) == G.VERIFY_FAIL
+    bad_s = bytearray(sigs)
+    j = n - 10
+    bad_s[192 * j:192 * (j + 2)] = sigs[192 * (j + 1):192 * (j + 2)] + sigs[192 * j:192 * (j + 1)]
+    bad_s = bytes(bad_s)
+    assert L.gbls_multi_verify_indexed(msgs, bad_s, idx_c, None, u64(rands), n) == G.VERIFY_FAIL
+    for (m_, s_, at) in ((bad_m, sigs, 700001 - 1000), (msgs, bad_s, n - 2048)):
+        b, e = at, at + 2048
+        pk_pts = F.public_keys([sks[int(i)] for i in idx[b:e]])
+        assert REF.ref_multi_verify(m_[32 * b:32 * e], s_[192 * b:192 * e], pk_pts, u64(rands[b:e]), e - b, 16) == 0
 
 
 # ------------------------------------------------------------------ C3

@@ -11,5 +11,5 @@ for p in ${2:?points}; do
   b=$(echo $p | cut -d: -f1); i=$(echo $p | cut -d: -f2); e=$(echo $p | cut -s -d: -f3 | tr , ' ')
   k=$((k + 1))
   echo "$p" > $O/point_$k.txt
-  env $e timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu --batches $b --inflight $i >> $O/point_$k.txt 2>&1 || exit 1
+  env $e timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu --tuning --batches $b --inflight $i >> $O/point_$k.txt 2>&1 || exit 1
 done
