@@ -221,7 +221,14 @@ HD void fp_from_be64_words(fp &r, const uint32_t *w) {
 // so t = t' nd^2, chi = delta t^2 = +-1 (delta's quadratic character), 1/t = chi delta t
 // and 1/nd = nd (t' / t) = chi nd t' t delta.  delta = 0 (only when a = 0) has no
 // character; that case falls back to the binary-GCD inversion.
-HD void fp2_sqrt_norm_inv(fp2 &r, fp &ndinv, const fp2 &a, const fp &gamma, const fp &nd) {
+// The exponentiation a^((p-3)/4) is a policy (Pow) so that the latency-regime kernel can
+// run it on a 16-lane row (bls_dfp.h) while the rest of the map stays per lane.
+struct LanePow {
+  HD void operator()(fp &r, const fp &a) const { fp_pow_pm3d4(r, a); }
+};
+template <class Pow>
+HD void fp2_sqrt_norm_inv(fp2 &r, fp &ndinv, const fp2 &a, const fp &gamma, const fp &nd,
+                          const Pow &pow) {
   fp delta, t, tp, x0, x0sq, tmp, nd2, u;
   fp_add(delta, a.c0, gamma);
   fp_half(delta, delta);
@@ -232,7 +239,7 @@ HD void fp2_sqrt_norm_inv(fp2 &r, fp &ndinv, const fp2 &a, const fp &gamma, cons
   fp_sqr(nd2, nd);
   fp_sqr(u, nd2);
   fp_mul(u, u, delta);     // delta nd^4
-  fp_pow_pm3d4(tp, u);     // t'
+  pow(tp, u);              // t'
   fp_mul(t, tp, nd2);      // t
   fp_mul(x0, delta, t);
   fp_sqr(x0sq, x0);
@@ -256,7 +263,8 @@ HD void fp2_sqrt_norm_inv(fp2 &r, fp &ndinv, const fp2 &a, const fp &gamma, cons
 
 // Simplified SWU on E2': y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2), inversion-free up to
 // one final Fp2 inversion, returning a Jacobian point on E2'.
-HD void map_to_curve_sswu(g2j &out, const fp2 &u) {
+template <class Pow>
+HD void map_to_curve_sswu(g2j &out, const fp2 &u, const Pow &pow) {
   const fp2 A = fp2_const(k::SSWU_A_C0, k::SSWU_A_C1);
   const fp2 B = fp2_const(k::SSWU_B_C0, k::SSWU_B_C1);
   const fp2 Z = fp2_const(k::SSWU_Z_C0, k::SSWU_Z_C1);
@@ -291,7 +299,7 @@ HD void map_to_curve_sswu(g2j &out, const fp2 &u) {
   fp_sqr(n, a1.c0);
   fp_sqr(nt, a1.c1);
   fp_add(n, n, nt);
-  fp_pow_pm3d4(gamma, n);
+  pow(gamma, n);
   fp_mul(gamma, gamma, n);  // n^((p+1)/4)
   fp_sqr(g2, gamma);
   bool is_sq = fp_eq(g2, n);
@@ -320,7 +328,7 @@ HD void map_to_curve_sswu(g2j &out, const fp2 &u) {
   fp_sqr(nd, D.c0);
   fp_sqr(ndt, D.c1);
   fp_add(nd, nd, ndt);
-  fp2_sqrt_norm_inv(s, ndinv, a, gsel, nd);
+  fp2_sqrt_norm_inv(s, ndinv, a, gsel, nd, pow);
   // affine: x = Nsel / D, y = s / D^2  (sgn0 needs the affine y); 1/D = conj(D) / N(D)
   fp2 Di, Di2, x, y;
   fp2_conj(Di, D);
@@ -414,11 +422,13 @@ HD void hash_to_field_g2(fp2 (&u)[2], const uint8_t *msg, uint32_t mlen, dst_ref
   fp_from_be64_words(u[1].c1, uni + 48);
 }
 // map_to_curve (SSWU + 3-isogeny) of one field element -> Jacobian point on E2
-HD void map_to_g2(g2j &q, const fp2 &u) {
+template <class Pow>
+HD void map_to_g2(g2j &q, const fp2 &u, const Pow &pow) {
   g2j m;
-  map_to_curve_sswu(m, u);
+  map_to_curve_sswu(m, u, pow);
   iso_map_g2(q, m);
 }
+HD void map_to_g2(g2j &q, const fp2 &u) { map_to_g2(q, u, LanePow()); }
 // hash_to_curve(msg) with DST, result as a Jacobian point on E2 (in G2).  The device
 // pipeline runs the same three stages as separate kernels (k_h2c_*).
 HD void hash_to_g2(g2j &r, const uint8_t *msg, uint32_t mlen, dst_ref dst) {

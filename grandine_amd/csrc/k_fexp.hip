@@ -3,6 +3,7 @@
 // exponentiation on the wave-cooperative Fp12 engine, and the verdict
 // (blst PAIRING_FinalVerify: result == 1, and no set flagged bad), inversion-free.
 #include "bls_wave12.h"
+#include "bls_w12d.h"
 #include "gbls_common.h"
 
 namespace gbls {
@@ -66,9 +67,75 @@ __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const in
   if (lane == 0) verdict[s] = (!bad && w12_is_fp6_image(A)) ? ST_SUCCESS : ST_VERIFY_FAIL;
 }
 
+// The same verdict on the row-distributed Fp12 engine (bls_w12d.h): one 56-row workgroup per
+// segment, every Fp12 product one row-product deep.  The latency form, for launches of a few
+// segments (blocks, gossip batches, C2 batches), where the one-wave form leaves the chip idle
+// behind a serial chain of ~350 Fp12 operations.  Partials are read as repacked limbs (an Fp*
+// scalar per partial, which the exponentiation removes).
+__global__ void __launch_bounds__(w12d::THREADS) k_final_verdict_d(const fp12 *part,
+                                                                   const int32_t *err,
+                                                                   uint32_t nparts, uint32_t nseg,
+                                                                   int32_t *verdict) {
+  __shared__ __attribute__((aligned(16))) uint32_t f[w12d::IMG], G[w12d::IMG], A[w12d::IMG],
+      B[w12d::IMG], T[w12d::IMG], X[w12d::IMG], ws[w12d::WS];
+  __shared__ int flags[12];
+  __shared__ int bad;
+  w12d::Eng e;
+  w12d::begin(e, ws);
+  const uint32_t s = blockIdx.x;
+  w12d::load_scaled(e, f, reinterpret_cast<const uint32_t *>(part + s));
+  if (threadIdx.x == 0) bad = err[s];
+  for (uint32_t k2 = 1; k2 < nparts; k2++) {
+    w12d::load_scaled(e, X, reinterpret_cast<const uint32_t *>(part + (size_t)k2 * nseg + s));
+    if (threadIdx.x == 0) bad |= err[(size_t)k2 * nseg + s];
+    w12d::mul(e, f, f, X);
+  }
+  w12d::zero_flags(e, flags, f, 0, 12);  // f = 0 (a degenerate Miller value) is rejected
+  if (threadIdx.x == 0) {
+    int all = 1;
+    for (int i = 0; i < 12; i++) all &= flags[i];
+    if (all) bad = 1;
+  }
+  // G = f^(p^2+1); A = G^(x-1); A = A^(x-1); B = A^(x+p); C = B^(x^2) frob2(B) conj(B);
+  // R = C G^3 (the k_final_verdict chain, same exponents)
+  w12d::frob2(e, G, f);
+  w12d::mul(e, G, G, f);
+  w12d::exp_x(e, A, G);
+  w12d::conj(e, X, G);
+  w12d::mul(e, A, A, X);
+  w12d::exp_x(e, B, A);
+  w12d::conj(e, X, A);
+  w12d::mul(e, A, B, X);
+  w12d::exp_x(e, B, A);
+  w12d::frob(e, X, A);
+  w12d::mul(e, B, B, X);
+  w12d::exp_x(e, T, B);
+  w12d::exp_x(e, A, T);
+  w12d::frob2(e, X, B);
+  w12d::mul(e, A, A, X);
+  w12d::conj(e, X, B);
+  w12d::mul(e, A, A, X);
+  w12d::mul(e, X, G, G);
+  w12d::mul(e, X, X, G);
+  w12d::mul(e, A, A, X);
+  w12d::zero_flags(e, flags, A, 6, 12);  // the w-half of R is zero: R in Fp6
+  if (threadIdx.x == 0) {
+    int fp6 = 1;
+    for (int i = 6; i < 12; i++) fp6 &= flags[i];
+    verdict[s] = (!bad && fp6) ? ST_SUCCESS : ST_VERIFY_FAIL;
+  }
+}
+
+// segments up to this many take the row-distributed (latency) form
+constexpr uint32_t kFinalRowsMaxSegs = 64;
+
 void launch_final_verdict(hipStream_t st, const fp12 *partials, const int32_t *err,
                           uint32_t nparts, uint32_t nseg, int32_t *verdict) {
-  if (nseg) k_final_verdict<<<nseg, 64, 0, st>>>(partials, err, nparts, nseg, verdict);
+  if (!nseg) return;
+  if (nseg <= kFinalRowsMaxSegs)
+    k_final_verdict_d<<<nseg, w12d::THREADS, 0, st>>>(partials, err, nparts, nseg, verdict);
+  else
+    k_final_verdict<<<nseg, 64, 0, st>>>(partials, err, nparts, nseg, verdict);
 }
 
 }  // namespace gbls

@@ -10,6 +10,7 @@
 //               Fp12 products (bls_wave12.h)
 //   k_ml_horner wave per segment: Horner over the 68 events, then conj (x < 0)
 #include "bls_wave12.h"
+#include "bls_w12d.h"
 #include "bls_field28.h"
 #include "gbls_common.h"
 
@@ -153,8 +154,42 @@ void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint3
   dim3 grid(nout, ML_EVENTS);
   if (nout) k_ml_reduce<<<grid, 64, 0, st>>>(Vin, nin, red, nout, Vout);
 }
+// k_ml_horner on the row-distributed Fp12 engine (bls_w12d.h), for launches of a few
+// segments: all 68 event values of the segment are staged in LDS first (52 KB), then the
+// 131-step chain runs one row-product per Fp12 product.  Event values are read as repacked
+// limbs (an Fp* scalar each; the final exponentiation removes them); the partial is written
+// as canonical engine-form words.
+__global__ void __launch_bounds__(w12d::THREADS) k_ml_horner_d(const fp12 *V, uint32_t nseg,
+                                                               fp12 *partial) {
+  __shared__ __attribute__((aligned(16))) uint32_t ev[ML_EVENTS * w12d::IMG], acc[w12d::IMG],
+      ws[w12d::WS];
+  w12d::Eng e;
+  w12d::begin(e, ws);
+  const uint32_t s = blockIdx.x;
+  for (uint32_t q = e.row; q < (uint32_t)ML_EVENTS * 12; q += w12d::ROWS) {
+    const uint32_t ev_i = q / 12, c = q % 12;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(V + (size_t)ev_i * nseg + s) + 12 * c;
+    ev[ev_i * w12d::IMG + 16 * c + e.j] = dfp::from_words_scaled(w);
+  }
+  __syncthreads();
+  w12d::copy(e, acc, ev);
+  for (int k = 1; k < ML_EVENTS; k++) {
+    if (ev_is_dbl(k)) w12d::mul(e, acc, acc, acc);
+    w12d::mul(e, acc, acc, ev + k * w12d::IMG);
+  }
+  w12d::conj(e, acc, acc);
+  w12d::store_words(e, reinterpret_cast<uint32_t *>(partial + s), acc);
+}
+
+// segments up to this many take the row-distributed (latency) form
+constexpr uint32_t kHornerRowsMaxSegs = 64;
+
 void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial) {
-  if (nseg) k_ml_horner<<<nseg, 64, 0, st>>>(V, nseg, partial);
+  if (!nseg) return;
+  if (nseg <= kHornerRowsMaxSegs)
+    k_ml_horner_d<<<nseg, w12d::THREADS, 0, st>>>(V, nseg, partial);
+  else
+    k_ml_horner<<<nseg, 64, 0, st>>>(V, nseg, partial);
 }
 
 }  // namespace gbls

@@ -21,7 +21,9 @@ def idx(h, j, k):
     return h * 6 + j * 2 + k
 
 
-def main():
+def build():
+    """(prod, post1, post2, post3): the 54 product operand sets and the three recombination
+    rounds as (value index, sign) lists (value space [p_0..p_53 | POST1 | POST2])."""
     # ---- products: (i6, j, k) with i6 in {0: a0*b0, 1: a1*b1, 2: (a0+a1)(b0+b1)},
     # j the Fp6 Karatsuba product, k the Fp2 Karatsuba product.
     fp6_sets = {0: [0], 1: [1], 2: [0, 1]}                 # w-parts summed
@@ -104,6 +106,12 @@ def main():
     for rnd in (post1, post2, post3):
         for terms in rnd:
             assert all(abs(s) == 1 for _, s in terms)
+    return prod, post1, post2, post3
+
+
+def main():
+    prod, post1, post2, post3 = build()
+    base1, base2 = 54, 90
 
     # ---- per-lane plan: the same maps as register-resident byte lists.  Positive terms
     # first, then negative ones, padded to the round's maxima with the zero slot, so that
