@@ -551,6 +551,30 @@ def bench_c1(args, L, G, F, np):
     conc = time.perf_counter() - t
     assert not errs
     glat.sort()
+    # f3: the block under gossip load -- 16 threads keep submitting 64-set batches while the
+    # block's finish runs with the block-import priority class (GBLS_CALL_BLOCK) and without
+    stop = threading.Event()
+
+    def loader():
+        while not stop.is_set():
+            if L.gbls_multi_verify(gm, gs, gp, r64, 64) != G.SUCCESS:
+                errs.append(1)
+
+    def finish_flags(flags):
+        st = G.i32_array(n)
+        return L.gbls_multi_verify_compressed_ex(msgs, comp_sigs, None, pidx, poff,
+                                                 (ctypes.c_uint64 * n)(*rands), n, st, flags)
+
+    ths = [threading.Thread(target=loader) for _ in range(nthr)]
+    for x in ths:
+        x.start()
+    time.sleep(0.05)
+    lat_prio = timed(lambda: finish_flags(G.CALL_BLOCK))
+    lat_noprio = timed(lambda: finish_flags(0))
+    stop.set()
+    for x in ths:
+        x.join()
+    assert not errs
     line = {"metric": "MultiVerifier::finish latency, mainnet-shaped block (C1)", "value": round(lat[len(lat) // 2] * 1e3, 3),
             "unit": "ms (p50)", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(sum(lat) / len(lat) * 1e3, 3), "higher_is_better": False, "scaling": "n/a",
@@ -564,6 +588,12 @@ def bench_c1(args, L, G, F, np):
             "gossip64": {"p50_ms": round(glat[len(glat) // 2] * 1e3, 3),
                          "p99_ms": round(glat[min(len(glat) - 1, int(len(glat) * 0.99))] * 1e3, 3),
                          "concurrent_16_threads_sets_per_s": round(nthr * per * 64 / conc, 1)},
+            "block_under_gossip_load": {
+                "block_priority_p50_ms": round(lat_prio[len(lat_prio) // 2] * 1e3, 3),
+                "block_priority_p99_ms": round(lat_prio[min(len(lat_prio) - 1, int(len(lat_prio) * 0.99))] * 1e3, 3),
+                "no_priority_p50_ms": round(lat_noprio[len(lat_noprio) // 2] * 1e3, 3),
+                "no_priority_p99_ms": round(lat_noprio[min(len(lat_noprio) - 1, int(len(lat_noprio) * 0.99))] * 1e3, 3),
+                "load": "16 threads x 64-set gbls_multi_verify in a loop"},
             "roofline": None, "cpu_baseline": None}
     print(json.dumps(line), flush=True)
 

@@ -47,6 +47,7 @@ VERIFY_FAIL = 5
 PK_IS_INFINITY = 6
 BAD_SCALAR = 7
 ERR_NO_DEVICE = 100
+CALL_BLOCK = 0x1  # gbls_multi_verify_compressed_ex: block-import priority class
 
 P1_BYTES = 96
 P2_BYTES = 192
@@ -72,6 +73,7 @@ EXPORTS = [
     "gbls_fast_aggregate_verify_indexed",
     "gbls_multi_verify_indexed",
     "gbls_multi_verify_compressed",
+    "gbls_multi_verify_compressed_ex",
     "gbls_multi_verify_bisect",
     "gbls_multi_verify_indexed_segments_device",
     "gbls_fast_aggregate_verify_indexed_device",
@@ -151,6 +153,8 @@ def load_library():
                 "gbls_fast_aggregate_verify_indexed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
                 "gbls_multi_verify_indexed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
                 "gbls_multi_verify_compressed": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+                "gbls_multi_verify_compressed_ex": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp,
+                                                               _c.c_uint32]),
                 "gbls_multi_verify_bisect": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
                 "gbls_fast_aggregate_verify_indexed_device": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp]),
                 "gbls_multi_verify_indexed_partials_device": (

@@ -128,9 +128,13 @@ struct StageTimer {  // RAII: events around one stage's launches when profiling
 struct Ctx {
   int hipdev = -1;
   hipStream_t own = nullptr, side1 = nullptr, side2 = nullptr;
+  // latency-regime streams on disjoint CU sets (created on first use, see cu_split): the
+  // main chain's waves never share a SIMD with the side streams' waves
+  hipStream_t own_m = nullptr, side1_m = nullptr, side2_m = nullptr;
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
              ev_done = nullptr, ev_upl = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool done_pending = false, upl_pending = false;
+  int cls = 0;                        // 0: normal, 1: block import (every stream high priority)
   bool active = false;                // a call holds the lease and has begun
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
   bool used = false;                  // last_stream is meaningful
@@ -146,15 +150,18 @@ struct Ctx {
   size_t stage_cap = 0, stage_used = 0;
   std::vector<uint32_t> host_tab;  // table assembly, reused across calls
 
-  bool init(int dev, bool side2_high, int prio_mode) {
+  bool init(int dev, bool side2_high, int prio_mode, int klass) {
     hipdev = dev;
+    cls = klass;
     HIPCHK(hipSetDevice(dev));
     // the hash_to_G2 -> lines chain is the critical path: its stream gets the highest
     // priority, the key-side and signature-side streams (slack of several ms) the lowest
     int least = 0, greatest = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     // prio_mode (GBLS_PRIO_MODE, experiments): 1 = every stream high, 2 = every stream low
-    const int pm = prio_mode, hi = pm == 2 ? least : greatest, lo = pm == 1 ? greatest : least;
+    // a block-import context (klass 1) runs all three streams at the highest priority
+    const int pm = klass ? 1 : prio_mode, hi = pm == 2 ? least : greatest,
+              lo = pm == 1 ? greatest : least;
     HIPCHK(hipStreamCreateWithPriority(&own, hipStreamNonBlocking, hi));
     HIPCHK(hipStreamCreateWithPriority(&side1, hipStreamNonBlocking, lo));
     HIPCHK(hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, side2_high ? hi : lo));
@@ -166,6 +173,21 @@ struct Ctx {
     HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_upl, hipEventDisableTiming));
+    return true;
+  }
+  // CU-masked stream triple: mode 1 = main chain on the first `main_cus` CUs, sides on the
+  // rest; mode 2 = the same split over interleaved CUs (CU i to the main chain when
+  // i % 4 != 3)
+  bool init_masked(int mode, int ncu) {
+    if (own_m) return true;
+    std::vector<uint32_t> mm((ncu + 31) / 32, 0), ms((ncu + 31) / 32, 0);
+    for (int i = 0; i < ncu; i++) {
+      bool main = mode == 1 ? i < ncu * 3 / 4 : (i % 4) != 3;
+      (main ? mm : ms)[i / 32] |= 1u << (i % 32);
+    }
+    HIPCHK(hipExtStreamCreateWithCUMask(&own_m, (uint32_t)mm.size(), mm.data()));
+    HIPCHK(hipExtStreamCreateWithCUMask(&side1_m, (uint32_t)ms.size(), ms.data()));
+    HIPCHK(hipExtStreamCreateWithCUMask(&side2_m, (uint32_t)ms.size(), ms.data()));
     return true;
   }
   // the call's main stream waits (on the GPU) for the previous call on this context;
@@ -245,6 +267,7 @@ constexpr uint32_t kMlRounds = 2;
 struct Device {
   int hipdev = -1;
   uint32_t nsimd = 1024;  // 4 SIMDs per CU
+  int ncu = 256;
   std::mutex mu;
   std::condition_variable cv;
   std::vector<Ctx *> idle;
@@ -266,6 +289,9 @@ struct Engine {
   uint32_t ml_rounds = kMlRounds;   // k_ml_group waves per SIMD for large launches
   bool side2_high = false;          // signature-side stream (MSM) at the main stream's priority
   int prio_mode = 0;                // 0: main high, sides low; 1: all high; 2: all low
+  int cu_split = 0;                 // latency-regime submissions on CU-masked streams (0: off)
+  uint32_t cu_split_max = 1024;     // ... up to this many sets
+  int leaders = 2;                  // coalescer leaders per device
 } g;
 
 // RAII lease of a context of one device: the idle context last used on the caller's
@@ -274,16 +300,16 @@ struct Engine {
 // recently used idle context (its reuse is ordered behind its previous call on the GPU)
 class Lease {
  public:
-  Lease(Device &d, bool affine, hipStream_t stream) : d_(d) {
+  Lease(Device &d, bool affine, hipStream_t stream, int cls = 0) : d_(d) {
     std::unique_lock<std::mutex> lk(d.mu);
     for (;;) {
       for (size_t i = 0; affine && !c_ && i < d.idle.size(); i++)
-        if (d.idle[i]->used && d.idle[i]->last_stream == stream) {
+        if (d.idle[i]->cls == cls && d.idle[i]->used && d.idle[i]->last_stream == stream) {
           c_ = d.idle[i];
           d.idle.erase(d.idle.begin() + i);
         }
       for (size_t i = 0; !c_ && i < d.idle.size(); i++)
-        if (d.idle[i]->idle_on_gpu()) {
+        if (d.idle[i]->cls == cls && d.idle[i]->idle_on_gpu()) {
           c_ = d.idle[i];
           d.idle.erase(d.idle.begin() + i);
         }
@@ -292,17 +318,19 @@ class Lease {
         c_ = d.all.back().get();
         fresh_ = true;
       }
-      if (!c_ && !d.idle.empty()) {
-        c_ = d.idle.front();
-        d.idle.erase(d.idle.begin());
-      }
+      for (size_t i = 0; !c_ && i < d.idle.size(); i++)
+        if (d.idle[i]->cls == cls) {
+          c_ = d.idle[i];
+          d.idle.erase(d.idle.begin() + i);
+        }
       if (c_) break;
-      d.cv.wait(lk);  // every context is leased: wait for one to come back
+      d.cv.wait(lk);  // every context of this class is leased: wait for one to come back
     }
     lk.unlock();
-    ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high, g.prio_mode) : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
+    ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high, g.prio_mode, cls)
+                 : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
   }
-  explicit Lease(Device &d) : Lease(d, false, nullptr) {}
+  explicit Lease(Device &d, int cls = 0) : Lease(d, false, nullptr, cls) {}
   ~Lease() {
     if (c_->active) {
       if (hipEventRecord(c_->ev_done, c_->cur) == hipSuccess) c_->done_pending = true;
@@ -315,7 +343,7 @@ class Lease {
       std::lock_guard<std::mutex> lk(d_.mu);
       d_.idle.push_back(c_);
     }
-    d_.cv.notify_one();
+    d_.cv.notify_all();  // waiters of either class
   }
   bool ok() const { return ok_; }
   Ctx &operator*() { return *c_; }
@@ -356,6 +384,10 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_PRIO_MODE")) g.prio_mode = std::atoi(e);
     if (const char *e = std::getenv("GBLS_ROW_CLEAR_MAX"))
       g_row_clear_max = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_CU_SPLIT")) g.cu_split = std::atoi(e);
+    if (const char *e = std::getenv("GBLS_CU_SPLIT_MAX"))
+      g.cu_split_max = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_LEADERS")) g.leaders = std::max(1, std::atoi(e));
 #ifdef GBLS_EXPERIMENTS
     if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
 #endif
@@ -370,6 +402,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
       g.devs.emplace_back(new Device());
       g.devs.back()->hipdev = id;
       g.devs.back()->nsimd = 4u * (uint32_t)prop.multiProcessorCount;
+      g.devs.back()->ncu = prop.multiProcessorCount;
     }
   }
   g.ready.store(true);
@@ -447,12 +480,20 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
                        int empty_is_error, fp12 *partials, int32_t *seg_err,
                        hipStream_t caller) {
   // The main chain runs on the context's high-priority stream; a caller stream (device
-  // entry points) hands over to it and waits for it at the end.
+  // entry points) hands over to it and waits for it at the end.  Small submissions may run
+  // on CU-masked streams (g.cu_split), the main chain apart from the side streams.
+  hipStream_t own = c.own, side1 = side1, side2 = side2;
+  if (g.cu_split && n <= g.cu_split_max) {
+    if (!c.init_masked(g.cu_split, d.ncu)) return false;
+    own = c.own_m;
+    side1 = c.side1_m;
+    side2 = c.side2_m;
+  }
   hipStream_t st = caller;
-  if (caller != c.own) {
+  if (caller != own) {
     HIPCHK(hipEventRecord(c.ev_in, caller));
-    HIPCHK(hipStreamWaitEvent(c.own, c.ev_in, 0));
-    st = c.own;
+    HIPCHK(hipStreamWaitEvent(own, c.ev_in, 0));
+    st = own;
   }
   bool single = !rands && n == nseg;  // one set per segment, r = 1
   for (size_t s = 0; single && s <= nseg; s++) single = seg_off[s] == s;
@@ -600,8 +641,8 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   int32_t *gpart_err = reinterpret_cast<int32_t *>(gpart + nchunks);
   // ---- fork
   HIPCHK(hipEventRecord(c.ev_fork, st));
-  HIPCHK(hipStreamWaitEvent(c.side1, c.ev_fork, 0));
-  HIPCHK(hipStreamWaitEvent(c.side2, c.ev_fork, 0));
+  HIPCHK(hipStreamWaitEvent(side1, c.ev_fork, 0));
+  HIPCHK(hipStreamWaitEvent(side2, c.ev_fork, 0));
   // main stream first: its first kernels reach the GPU before the side streams' floods
   {
     StageTimer t(S_H2C_FIELD, st);
@@ -613,45 +654,45 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   }
   const g1a *pks = nullptr;
   const int32_t *pre = nullptr;
-  if (!resolve_pks(c, d, src, n, c.side1, &pks, &pre)) return false;
-  HIPCHK(hipEventRecord(c.ev_pks, c.side1));
+  if (!resolve_pks(c, d, src, n, side1, &pks, &pre)) return false;
+  HIPCHK(hipEventRecord(c.ev_pks, side1));
   {
-    StageTimer t(S_G1MUL, c.side1);
-    launch_mv_g1mul(c.side1, pks, rands, N, c.P.as<g1s>());
+    StageTimer t(S_G1MUL, side1);
+    launch_mv_g1mul(side1, pks, rands, N, c.P.as<g1s>());
   }
   const int32_t *pre2 = nullptr;
   if (c.sig_c) {  // MultiVerifier::finish's decompression, inside this submission
     // sigs is then the lease's own output buffer (c.sigd, enqueue_host_batch)
-    launch_g2_decompress(c.side2, c.sig_c, N, const_cast<g2a *>(sigs), c.sig_st);
+    launch_g2_decompress(side2, c.sig_c, N, const_cast<g2a *>(sigs), c.sig_st);
     pre2 = c.sig_st;
     c.sig_c = nullptr;
     c.sig_st = nullptr;
   } else if (sig_groupcheck) {
-    launch_g2_check(c.side2, sigs, N, c.pre2.as<int32_t>(), 0);
+    launch_g2_check(side2, sigs, N, c.pre2.as<int32_t>(), 0);
     pre2 = c.pre2.as<int32_t>();
   }
   if (msm) {  // the keys' flags are read by the first MSM kernel
-    HIPCHK(hipStreamWaitEvent(c.side2, c.ev_pks, 0));
-    StageTimer t(S_MSM, c.side2);
-    launch_msm(c.side2, mp, c.msm.as<uint8_t>(), sigs, rands, pks, pre, pre2, N, T + segoff_at,
+    HIPCHK(hipStreamWaitEvent(side2, c.ev_pks, 0));
+    StageTimer t(S_MSM, side2);
+    launch_msm(side2, mp, c.msm.as<uint8_t>(), sigs, rands, pks, pre, pre2, N, T + segoff_at,
                empty_is_error, c.H.as<g2a>(), c.P.as<g1s>(), seg_err);
   } else if (!single) {
-    StageTimer t(S_G2MUL, c.side2);
-    launch_mv_g2mul(c.side2, sigs, rands, N, c.R.as<g2j>());
+    StageTimer t(S_G2MUL, side2);
+    launch_mv_g2mul(side2, sigs, rands, N, c.R.as<g2j>());
   }
   if (!msm) {
-    HIPCHK(hipStreamWaitEvent(c.side2, c.ev_pks, 0));
-    StageTimer t(S_G2SUM, c.side2);
+    HIPCHK(hipStreamWaitEvent(side2, c.ev_pks, 0));
+    StageTimer t(S_G2SUM, side2);
     if (single)
-      launch_single_S(c.side2, sigs, pks, pre, pre2, N, c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
+      launch_single_S(side2, sigs, pks, pre, pre2, N, c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
     else
-      launch_g2sum(c.side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
+      launch_g2sum(side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
                    T + segoff_at, NS, N, pks, rands, pre, pre2, empty_is_error, gpart, gpart_err,
                    c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
   }
   {  // the extra pairs' lines of the first event slice (all events when not sliced)
-    StageTimer t(S_LINES_S, c.side2);
-    launch_lines(c.side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, EC, c.Ts.as<g2h>(),
+    StageTimer t(S_LINES_S, side2);
+    launch_lines(side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, EC, c.Ts.as<g2h>(),
                  c.lines.as<uint32_t>());
   }
   {
@@ -662,8 +703,8 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     StageTimer t(S_LINES, st);
     launch_lines(st, c.H.as<g2a>(), 0, N, NP, 0, EC, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
   }
-  HIPCHK(hipEventRecord(c.ev_side1, c.side1));
-  HIPCHK(hipEventRecord(c.ev_side2, c.side2));
+  HIPCHK(hipEventRecord(c.ev_side1, side1));
+  HIPCHK(hipEventRecord(c.ev_side2, side2));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side1, 0));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
   for (int e0 = 0; e0 < ML_EVENTS; e0 += EC) {
@@ -803,7 +844,7 @@ bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
 // the device with their statuses written to sig_status.
 bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, int32_t *sig_status,
                  const PkSource &src, const uint64_t *rands, size_t n, const uint32_t *seg_off,
-                 size_t nseg, int32_t *verdicts) {
+                 size_t nseg, int32_t *verdicts, int cls = 0) {
   std::shared_lock<std::shared_mutex> rl(g.reg_mu);
   const size_t ndev = g.devs.size();
   // ---- one large batch: per-device Miller partials, one final exponentiation
@@ -816,7 +857,7 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
     for (size_t j = 0; j < k && ok; j++) {
       size_t b = n * j / k, e = n * (j + 1) / k;
       Device &d = *g.devs[j];
-      leases.emplace_back(new Lease(d));
+      leases.emplace_back(new Lease(d, cls));
       Lease &L = *leases.back();
       uint32_t seg[2] = {0, (uint32_t)(e - b)};
       ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, sigs_c, sig_status, src, rands, b, e,
@@ -827,7 +868,7 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
     leases.clear();
     if (!ok) return false;
     Device &d0 = *g.devs[0];
-    Lease L(d0);
+    Lease L(d0, cls);
     if (!L.ok() || !L->begin(L->own)) return false;
     hipStream_t st = L->own;
     if (!L->upload_staged(L->in0, parts.data(), k * sizeof(fp12), st) ||
@@ -859,7 +900,7 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
     segs[j].resize(s1 - s0 + 1);
     for (size_t s = s0; s <= s1; s++) segs[j][s - s0] = seg_off[s] - (uint32_t)b;
     Device &d = k == 1 ? pick_device() : *g.devs[j];
-    leases.emplace_back(new Lease(d));
+    leases.emplace_back(new Lease(d, cls));
     Lease &L = *leases.back();
     ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, sigs_c, sig_status, src, rands, b, e,
                                       segs[j].data(), s1 - s0, verdicts + s0, nullptr, nullptr);
@@ -872,13 +913,20 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
 // ----- f3: cross-caller coalescing.  Concurrent host-pointer multi_verify calls (the
 // node's gossip batches of <= 64 sets, p2p/src/attestation_verifier.rs:37,142-163, and
 // the block verification pool's per-block batches, p2p/src/block_verification_pool.rs:
-// 103-128) queue here; a caller that finds fewer than kLeadersPerDevice x devices
+// 103-128) queue here; a caller that finds fewer than g.leaders x devices
 // submissions in flight becomes a leader and verifies every queued request with the same
 // key source kind as ONE segmented submission (each request keeps its own segments and
 // verdicts).  Batches therefore grow with the load, while an idle engine runs a lone
 // call immediately (no waiting window).
-constexpr int kLeadersPerDevice = 2;
-constexpr size_t kMaxMergedSets = 1 << 20;
+// merged gossip submissions stay below one C2 step (~17 ms of GPU time), so a block-import
+// submission never waits long behind one
+constexpr size_t kMaxMergedSets = 1 << 16;
+// Block import (GBLS_CALL_BLOCK, transition_functions/src/deneb/state_transition.rs:69-71
+// verifies a block's signatures on the critical path of its import) has its own queue and
+// leader slot per device: it never waits for a normal leader, is merged only with other
+// block requests up to kPrioMaxSets sets (the latency cap), and runs on contexts whose
+// streams all have the highest priority.
+constexpr size_t kPrioMaxSets = 8192;
 
 struct CoReq {
   const uint8_t *msgs;
@@ -891,6 +939,7 @@ struct CoReq {
   int32_t *verdicts;
   const uint8_t *sigs_c = nullptr;  // compressed signatures instead of sigs (96 B each)
   int32_t *sig_status = nullptr;    // their decompression statuses (with sigs_c)
+  int prio = 0;                     // 1: block import
   bool done = false, ok = false;
   int err = GBLS_ERR_NONE;
   int kind() const { return (src.pts ? 1 : 0) | (src.off ? 2 : 0) | (sigs_c ? 4 : 0); }
@@ -900,19 +949,19 @@ struct CoReq {
 struct Coalescer {
   std::mutex mu;
   std::condition_variable cv;
-  std::vector<CoReq *> q;
-  int leaders = 0;
+  std::vector<CoReq *> q, pq;  // normal and block-import queues
+  int leaders = 0, pleaders = 0;
 } co;
 
 bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, int32_t *sig_status,
                  const PkSource &src, const uint64_t *rands, size_t n, const uint32_t *seg_off,
-                 size_t nseg, int32_t *verdicts);
+                 size_t nseg, int32_t *verdicts, int cls);
 
 void run_merged(std::vector<CoReq *> &batch) {
   if (batch.size() == 1) {
     CoReq &r = *batch[0];
     r.ok = verify_host(r.msgs, r.sigs, r.sigs_c, r.sig_status, r.src, r.rands, r.n, r.seg_off,
-                       r.nseg, r.verdicts);
+                       r.nseg, r.verdicts, r.prio);
     r.err = t_last_error;
     return;
   }
@@ -958,7 +1007,7 @@ void run_merged(std::vector<CoReq *> &batch) {
   if (r0.src.off) src.off = off.data();
   bool ok = verify_host(msgs.data(), r0.sigs_c ? nullptr : sigs.data(),
                         r0.sigs_c ? sigc.data() : nullptr, r0.sigs_c ? sst.data() : nullptr, src,
-                        rands.data(), n, seg.data(), nseg, v.data());
+                        rands.data(), n, seg.data(), nseg, v.data(), r0.prio);
   int err = t_last_error;
   sat = 0;
   at = 0;
@@ -975,29 +1024,33 @@ void run_merged(std::vector<CoReq *> &batch) {
 bool coalesced_verify(CoReq &r) {
   if (!g.coalesce.load()) {
     bool ok = verify_host(r.msgs, r.sigs, r.sigs_c, r.sig_status, r.src, r.rands, r.n, r.seg_off,
-                          r.nseg, r.verdicts);
+                          r.nseg, r.verdicts, r.prio);
     return ok;
   }
-  const int max_leaders = kLeadersPerDevice * (int)g.devs.size();
+  const int ndev = (int)g.devs.size();
+  const int max_leaders = (r.prio ? 1 : g.leaders) * ndev;
+  const size_t cap = r.prio ? kPrioMaxSets : kMaxMergedSets;
+  std::vector<CoReq *> &q = r.prio ? co.pq : co.q;
+  int &leaders = r.prio ? co.pleaders : co.leaders;
   std::unique_lock<std::mutex> lk(co.mu);
-  co.q.push_back(&r);
+  q.push_back(&r);
   while (!r.done) {
-    if (co.leaders < max_leaders && !co.q.empty()) {
-      co.leaders++;
+    if (leaders < max_leaders && !q.empty()) {
+      leaders++;
       std::vector<CoReq *> batch;
-      auto mine = std::find(co.q.begin(), co.q.end(), &r);
-      int kind = mine != co.q.end() ? r.kind() : co.q.front()->kind();
+      auto mine = std::find(q.begin(), q.end(), &r);
+      int kind = mine != q.end() ? r.kind() : q.front()->kind();
       size_t sets = 0;
-      if (mine != co.q.end()) {
+      if (mine != q.end()) {
         batch.push_back(&r);
         sets = r.n;
-        co.q.erase(mine);
+        q.erase(mine);
       }
-      for (auto it = co.q.begin(); it != co.q.end();) {
-        if ((*it)->kind() == kind && (batch.empty() || sets + (*it)->n <= kMaxMergedSets)) {
+      for (auto it = q.begin(); it != q.end();) {
+        if ((*it)->kind() == kind && (batch.empty() || sets + (*it)->n <= cap)) {
           sets += (*it)->n;
           batch.push_back(*it);
-          it = co.q.erase(it);
+          it = q.erase(it);
         } else {
           ++it;
         }
@@ -1006,7 +1059,7 @@ bool coalesced_verify(CoReq &r) {
       run_merged(batch);  // writes verdicts, ok, err; `done` is published under co.mu
       lk.lock();
       for (CoReq *b : batch) b->done = true;
-      co.leaders--;
+      leaders--;
       co.cv.notify_all();
     } else {
       co.cv.wait(lk);
@@ -1070,7 +1123,7 @@ bool bisect_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
     }
     std::vector<int32_t> v(pieces.size(), FAILED);
     if (!verify_host(gm.data(), gs.data(), nullptr, nullptr, s2, gr.data(), gs.size(), seg.data(),
-                     pieces.size(), v.data()))
+                     pieces.size(), v.data(), 0))
       return false;
     frontier.clear();
     for (size_t j = 0; j < pieces.size(); j++) {
@@ -1399,10 +1452,10 @@ int gbls_multi_verify_indexed(const uint8_t (*msgs)[32], const gbls_p2_affine *s
   return v;
 }
 
-int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
-                                 const gbls_p1_affine *pks, const uint32_t *pk_idx,
-                                 const uint32_t *pk_off, const uint64_t *rands, size_t n,
-                                 int32_t *sig_status) {
+int gbls_multi_verify_compressed_ex(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
+                                    const gbls_p1_affine *pks, const uint32_t *pk_idx,
+                                    const uint32_t *pk_off, const uint64_t *rands, size_t n,
+                                    int32_t *sig_status, uint32_t call_flags) {
   if (!sig_status) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
   fill(sig_status, n, GBLS_BAD_ENCODING);
   API_BEGIN
@@ -1417,6 +1470,7 @@ int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs
   r.src.off = pk_off;
   r.sigs_c = &sigs[0][0];
   r.sig_status = sig_status;
+  r.prio = (call_flags & GBLS_CALL_BLOCK) ? 1 : 0;
   if (!coalesced_verify(r)) {
     fill(sig_status, n, GBLS_BAD_ENCODING);
     return GBLS_VERIFY_FAIL;
@@ -1424,6 +1478,13 @@ int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs
   for (size_t i = 0; i < n; i++)  // MultiVerifier::finish: a decoding error comes first
     if (sig_status[i] != GBLS_SUCCESS) return sig_status[i];
   return v;
+}
+
+int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
+                                 const gbls_p1_affine *pks, const uint32_t *pk_idx,
+                                 const uint32_t *pk_off, const uint64_t *rands, size_t n,
+                                 int32_t *sig_status) {
+  return gbls_multi_verify_compressed_ex(msgs, sigs, pks, pk_idx, pk_off, rands, n, sig_status, 0);
 }
 
 int gbls_multi_verify_bisect(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,

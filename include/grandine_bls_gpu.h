@@ -27,6 +27,8 @@
  *   gbls_multi_verify_indexed   multi_verify / Triple::verify_aggregate over registry indices
  *   gbls_multi_verify_compressed  MultiVerifier::finish in one submission: signature
  *                               decompression (verifier.rs:309-313) fused into the batch verify
+ *   gbls_multi_verify_compressed_ex  the same with a priority class (block import,
+ *                               transition_functions/src/deneb/state_transition.rs:69-71)
  *   gbls_g1_aggregate_indexed   AggregatePublicKey::aggregate over registry indices (e.g. the
  *                               512-key get_next_sync_committee aggregate,
  *                               helper_functions/src/accessors.rs:605-628)
@@ -192,6 +194,17 @@ int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs
                                  const gbls_p1_affine *pks, const uint32_t *pk_idx,
                                  const uint32_t *pk_off, const uint64_t *rands, size_t n,
                                  int32_t *sig_status);
+/* f3 priority class.  call_flags & GBLS_CALL_BLOCK marks block import (the block's
+ * MultiVerifier::finish, which transition_functions/src/deneb/state_transition.rs:69-71 runs
+ * on the critical path of importing it): the call has its own queue and leader slot per
+ * device, so it never waits behind merged gossip submissions (themselves capped at 65536
+ * sets), is merged only with other block calls (up to 8192 sets), and runs on streams of
+ * the highest priority.  Otherwise identical to gbls_multi_verify_compressed. */
+#define GBLS_CALL_BLOCK 0x1u
+int gbls_multi_verify_compressed_ex(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
+                                    const gbls_p1_affine *pks, const uint32_t *pk_idx,
+                                    const uint32_t *pk_off, const uint64_t *rands, size_t n,
+                                    int32_t *sig_status, uint32_t call_flags);
 /* f2: per-set verdicts (GBLS_SUCCESS / GBLS_VERIFY_FAIL, as each set would fare in
  * multi_verify alone) by GPU bisection: the batch, then rounds that split every failing
  * range 16 ways and verify all pieces as segments of one submission.  Keys come from

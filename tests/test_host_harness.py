@@ -12,6 +12,11 @@ from oracle import bls12_381 as O
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
 SO = os.path.join(ROOT, "tests", "native", "_build", "libhost_harness.so")
+# GBLS_HARNESS_SAN=1 (tests/test_host_sanitizers.py): an ASan + UBSan build of the same harness,
+# loaded by a child interpreter that preloads libasan
+SAN = os.environ.get("GBLS_HARNESS_SAN") == "1"
+if SAN:
+    SO = os.path.join(ROOT, "tests", "native", "_build", "libhost_harness_san.so")
 RINV = pow(1 << 384, -1, O.P)
 
 
@@ -27,7 +32,9 @@ def H():
     # GBLS_HARNESS_DEFS: extra -D flags, to check an experiment build's arithmetic (e.g.
     # -DGBLS_POW_ENGINE) with the same tests
     defs = os.environ.get("GBLS_HARNESS_DEFS", "").split()
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-D__HIP_PLATFORM_AMD__",
+    opt = (["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
+           if SAN else ["-O2"])
+    subprocess.check_call(["g++"] + opt + ["-std=c++17", "-shared", "-fPIC", "-D__HIP_PLATFORM_AMD__",
                            "-I/opt/rocm/include"] + defs + ["-o", SO, src])
     L = ctypes.CDLL(SO)
     L.h_multi_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
