@@ -482,7 +482,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   // The main chain runs on the context's high-priority stream; a caller stream (device
   // entry points) hands over to it and waits for it at the end.  Small submissions may run
   // on CU-masked streams (g.cu_split), the main chain apart from the side streams.
-  hipStream_t own = c.own, side1 = side1, side2 = side2;
+  hipStream_t own = c.own, side1 = c.side1, side2 = c.side2;
   if (g.cu_split && n <= g.cu_split_max) {
     if (!c.init_masked(g.cu_split, d.ncu)) return false;
     own = c.own_m;
