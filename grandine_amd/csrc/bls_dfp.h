@@ -223,8 +223,8 @@ __device__ __forceinline__ uint32_t from_words_scaled(const uint32_t *w) {
 }
 // This form -> canonical engine-form words (x 2^384 mod p, < p): the row multiplies by
 // 2^384 mod p, every lane gathers and normalizes the limbs, subtracts p once if needed, and
-// lanes 0..11 store word j.
-__device__ __forceinline__ void to_words(uint32_t *w, uint32_t x, const Tabs &t) {
+// lane j < 12 returns word j (the other lanes return 0).
+__device__ __forceinline__ uint32_t word_of(uint32_t x, const Tabs &t) {
   const uint32_t r = mul(x, konst(K_COUT), t);
   uint32_t l[16];
   For<0, 16>::run([&](auto I) {
@@ -250,18 +250,22 @@ __device__ __forceinline__ void to_words(uint32_t *w, uint32_t x, const Tabs &t)
   const bool ge = br == 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) l[i] = ge ? d[i] : l[i];
-  // 28-bit limbs -> 32-bit words; lane j < 12 stores word j
+  // 28-bit limbs -> 32-bit words; lane j < 12 takes word j
   const uint32_t j = t.j;
+  uint32_t word = 0;
   if (j < 12) {
-    uint32_t word = 0;
 #pragma unroll
     for (int i = 0; i < 14; i++) {
       const int lo_bit = 28 * i - 32 * (int)j;  // position of limb i inside word j
       if (lo_bit > -28 && lo_bit < 32)
         word |= lo_bit >= 0 ? (l[i] << lo_bit) : (l[i] >> -lo_bit);
     }
-    w[j] = word;
   }
+  return word;
+}
+__device__ __forceinline__ void to_words(uint32_t *w, uint32_t x, const Tabs &t) {
+  const uint32_t word = word_of(x, t);
+  if (t.j < 12) w[t.j] = word;
 }
 
 // The row form (x 2^448) of an engine-form value held IN REGISTERS by every lane of the row

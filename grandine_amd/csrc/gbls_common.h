@@ -23,6 +23,9 @@ constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
 // ... and Miller lines of up to this many pairs run on 16-lane DPP rows (bls_gang.h),
 // 16 x 4096 lanes being one wave per SIMD
 constexpr uint32_t kRowRegimeMax = 6144;
+// ... and the smallest launches run one wave per point (bls_w4.h): cofactor clearing and
+// Miller lines of up to this many points
+constexpr uint32_t kW4Max = 1024;
 constexpr uint32_t kRowClearMax = 4096;  // cofactor clearing on rows (up to one C2 batch)
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
 extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic (GBLS_ML_R28)

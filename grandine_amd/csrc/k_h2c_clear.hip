@@ -7,6 +7,7 @@
 // (k_h2c_clear_lane: a quarter of the instructions per message, the chip already full).
 #include "gbls_common.h"
 #include "bls_gang.h"
+#include "bls_w4.h"
 
 namespace gbls {
 
@@ -91,9 +92,26 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n,
   H[i] = o;
 }
 
+// one wave per message (bls_w4.h: four row-distributed products per round), the smallest
+// launches: Q0 + Q1, the cofactor clearing and the affine conversion at ~0.5 us per round
+__global__ void __launch_bounds__(64) k_h2c_clear_w4(const g2j *Q, uint32_t n, g2a *H) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;  // whole waves
+  w4::Ctx c;
+  w4::init(c);
+  w4::J a, b, h;
+  w4::load(c, a, Q[2 * i]);
+  w4::load(c, b, Q[2 * i + 1]);
+  w4::add(c, a, a, b);
+  w4::clear_cofactor(c, h, a);
+  w4::store_affine(c, H + i, h);
+}
+
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   if (!n) return;
-  if (n >= kLaneRegimeClear)
+  if (n <= kW4Max)
+    k_h2c_clear_w4<<<n, 64, 0, st>>>(Q, n, H);
+  else if (n >= kLaneRegimeClear)
     k_h2c_clear_lane<<<nblk(n), WG, 0, st>>>(Q, n, H);
   else if (n <= g_row_clear_max)
     k_h2c_clear_row<<<nblk((size_t)n * 16), WG, 0, st>>>(Q, n, H);

@@ -9,6 +9,7 @@
 #include "gbls_common.h"
 #define GBLS_GANG_LINES
 #include "bls_gang.h"
+#include "bls_w4.h"
 
 namespace gbls {
 
@@ -116,10 +117,71 @@ __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first,
   lines_range(L, np, first + i, Q, e0, e1, Ts);
 }
 
+// one wave per pair (bls_w4.h), the smallest launches: a doubling step is six rounds of four
+// row-distributed products, the six line words two more (canonical engine form, SoA as above)
+__device__ __forceinline__ void line_put_w4(const w4::Ctx &c, uint32_t *L, uint32_t np, uint32_t pair,
+                                            int e, const w4::f2 &l0, const w4::f2 &l2, const w4::f2 &l3) {
+  const uint32_t j = c.t.j;
+  uint32_t w = dfp::word_of(w4::sel(c, l0.c0, l0.c1, l2.c0, l2.c1), c.t);
+  if (j < 12) L[line_word(e, (int)c.r, (int)j, np, pair)] = w;
+  w = dfp::word_of(w4::sel(c, l3.c0, l3.c1, l3.c0, l3.c1), c.t);
+  if (j < 12 && c.r < 2) L[line_word(e, 4 + (int)c.r, (int)j, np, pair)] = w;
+}
+__global__ void __launch_bounds__(64) k_lines_w4(const g2a *H, uint32_t first, uint32_t count,
+                                                 uint32_t np, int e0, int e1, g2h *Ts, uint32_t *L) {
+  const uint32_t i = blockIdx.x;
+  if (i >= count) return;  // whole waves
+  const uint32_t pair = first + i;
+  const g2a Q = H[pair];
+  const uint32_t j = threadIdx.x & 15, r = (threadIdx.x >> 4) & 3;
+  if (aff_is_inf(Q)) {  // identity lines: L0 = 1, L2 = L3 = 0
+    uint32_t one = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) one = j == (uint32_t)k ? k::ONE_M[k] : one;
+    for (int e = e0; e < e1; e++)
+      for (uint32_t cc = r; cc < 6; cc += 4)
+        if (j < 12) L[line_word(e - e0, (int)cc, (int)j, np, pair)] = cc == 0 ? one : 0u;
+    return;
+  }
+  w4::Ctx c;
+  w4::init(c);
+  w4::A2 q;
+  w4::load(c, q, Q);
+  w4::J T;
+  if (e0 > 0) {
+    g2j tj;
+    tj.x = Ts[pair].x;
+    tj.y = Ts[pair].y;
+    tj.z = Ts[pair].z;
+    w4::load(c, T, tj);
+  } else {
+    T.x = q.x;
+    T.y = q.y;
+    T.z = {c.one, 0u};
+  }
+  for (int e = e0; e < e1; e++) {
+    w4::f2 l0, l2, l3;
+    if (ev_is_dbl(e))
+      w4::line_dbl(c, T, l0, l2, l3);
+    else
+      w4::line_add_aff(c, T, q, l0, l2, l3);
+    line_put_w4(c, L, np, pair, e - e0, l0, l2, l3);
+  }
+  if (e1 < ML_EVENTS) {
+    g2h *o = Ts + pair;
+    w4::store4(c, T.x.c0, T.x.c1, T.y.c0, T.y.c1, o->x.c0.l, o->x.c1.l, o->y.c0.l, o->y.c1.l);
+    uint32_t w = dfp::word_of(w4::sel(c, T.z.c0, T.z.c1, T.z.c0, T.z.c1), c.t);
+    if (j < 12 && r == 0) o->z.c0.l[j] = w;
+    if (j < 12 && r == 1) o->z.c1.l[j] = w;
+  }
+}
+
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
                   int e0, int e1, g2h *Ts, uint32_t *lines) {
   if (!count) return;
-  if (count >= kLaneRegimeLines)
+  if (count <= kW4Max)
+    k_lines_w4<<<count, 64, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
+  else if (count >= kLaneRegimeLines)
     k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
   else if (count <= kRowRegimeMax)
     k_lines_row<<<nblk((size_t)count * 16), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);

@@ -6,6 +6,7 @@
 // workgroup tree.
 #include "gbls_common.h"
 #include "bls_gang.h"
+#include "bls_w4.h"
 
 namespace gbls {
 
@@ -225,8 +226,92 @@ void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint
   else
     k_mv_g1mul<<<nblk(4 * (size_t)n), WG, 0, st>>>(pks, rands, n, P);
 }
+// the same halves, one wave per (set, half) (bls_w4.h): a doubling is four rounds of four
+// row-distributed products, a mixed addition eight -- the latency regime
+__global__ void __launch_bounds__(64) k_mv_g2mul_w4(const g2a *sigs, const uint64_t *rands,
+                                                    uint32_t n, g2j *R) {
+  const uint32_t t = blockIdx.x;
+  if (t >= 2 * n) return;  // whole waves
+  const uint32_t i = t < n ? t : t - n;
+  const uint64_t r = rands ? rands[i] : 1;
+  const uint64_t k = t < n ? (r & 0xffffffffull) : (r >> 32);
+  const g2a base = sigs[i];
+  const uint32_t j = threadIdx.x & 15;
+  if (k == 0 || aff_is_inf(base)) {  // identity (jac_set_inf)
+    if (threadIdx.x < 12) {
+      uint32_t one = 0;
+#pragma unroll
+      for (int q = 0; q < 12; q++) one = j == (uint32_t)q ? k::ONE_M[q] : one;
+      R[t].x.c0.l[j] = one;
+      R[t].x.c1.l[j] = 0;
+      R[t].y.c0.l[j] = one;
+      R[t].y.c1.l[j] = 0;
+      R[t].z.c0.l[j] = 0;
+      R[t].z.c1.l[j] = 0;
+    }
+    return;
+  }
+  w4::Ctx c;
+  w4::init(c);
+  w4::A2 b;
+  w4::load(c, b, base);
+  w4::J acc;
+  acc.x = b.x;
+  acc.y = b.y;
+  acc.z = {c.one, 0u};
+  const int top = 63 - __clzll((long long)k);
+  for (int bit = top - 1; bit >= 0; bit--) {
+    w4::dbl(c, acc, acc);
+    if ((k >> bit) & 1) w4::madd(c, acc, acc, b);
+  }
+  w4::store_jac(c, R + t, acc);
+}
+
+// level 2 on one wave per segment (bls_w4.h): the segment's chunk partials in sequence, the
+// 2^32 shift of the high half (32 doublings) and the affine conversion, ~0.3 ms instead of the
+// quads' ~0.6 ms (their one-lane inversion dominates)
+__global__ void __launch_bounds__(64) k_g2sum_final_w4(const g2j *part, const int32_t *part_err,
+                                                       const uint32_t *chunks, const uint32_t *seg_chunk,
+                                                       const uint32_t *seg_off, uint32_t nseg, uint32_t n,
+                                                       int empty_is_error, g1s *P, g2a *H,
+                                                       int32_t *seg_err) {
+  const uint32_t s = blockIdx.x;
+  if (s >= nseg) return;
+  w4::Ctx c;
+  w4::init(c);
+  w4::J lo, hi;
+  w4::set_inf(c, lo);
+  w4::set_inf(c, hi);
+  int32_t err = 0;
+  for (uint32_t q = seg_chunk[s]; q < seg_chunk[s + 1]; q++) {
+    w4::J v;
+    w4::load(c, v, part[q]);
+    if (chunks[4 * q + 1] == 0)
+      w4::add(c, lo, lo, v);
+    else
+      w4::add(c, hi, hi, v);
+    err |= part_err[q];
+  }
+  if (empty_is_error && seg_off[s + 1] == seg_off[s]) err = 1;
+  for (int d = 0; d < 32; d++) w4::dbl(c, hi, hi);
+  w4::add(c, lo, lo, hi);
+  w4::store_affine(c, H + n + s, lo);
+  if (threadIdx.x == 0) {
+    g1s ng1;
+    fp_set(ng1.x, k::G1X_M);
+    fp_set(ng1.y, k::G1NEGY_M);
+    fp_one(ng1.c);
+    P[n + s] = ng1;
+    seg_err[s] = err;
+  }
+}
+
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R) {
-  if (n) k_mv_g2mul<<<nblk(8 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
+  if (!n) return;
+  if (2 * n <= kW4Max)
+    k_mv_g2mul_w4<<<2 * n, 64, 0, st>>>(sigs, rands, n, R);
+  else
+    k_mv_g2mul<<<nblk(8 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
 }
 void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t nchunks,
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
@@ -235,7 +320,10 @@ void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t
                   int32_t *seg_err) {
   if (nchunks)
     k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, rands, pre, pre2, part, part_err);
-  if (nseg)
+  if (nseg && nseg <= kW4Max)
+    k_g2sum_final_w4<<<nseg, 64, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n,
+                                          empty_is_error, P, H, seg_err);
+  else if (nseg)
     k_g2sum_final<<<nseg, WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n,
                                        empty_is_error, P, H, seg_err);
 }

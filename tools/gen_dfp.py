@@ -96,6 +96,11 @@ def f2_pow(a, e):
     return r
 
 
+def f2_inv(a):
+    n = pow(a[0] * a[0] + a[1] * a[1], P - 2, P)
+    return (a[0] * n % P, -a[1] * n % P)
+
+
 def main():
     pinv = (-pow(P, -1, R)) % R
     pl, pp = limbs(P), limbs(pinv)
@@ -103,6 +108,11 @@ def main():
     frob1 = [f2_pow(xi, e * (P - 1) // 6) for e in range(6)]
     frob2 = [f2_pow(xi, e * (P * P - 1) // 6) for e in range(6)]
     assert all(f[1] == 0 for f in frob2)
+    cx = f2_inv(f2_pow(xi, (P - 1) // 3))
+    cy = f2_inv(f2_pow(xi, (P - 1) // 2))
+    psi2x = f2_mul((cx[0], -cx[1] % P), cx)
+    psi2y = f2_mul((cy[0], -cy[1] % P), cy)
+    assert cx[0] == 0 and psi2x[1] == 0 and psi2y[1] == 0
     consts = {
         "P": limbs(P),
         "CIN": limbs(pow(2, 2 * N * W - 384, P)),   # engine form (x 2^384) -> x 2^448
@@ -114,6 +124,13 @@ def main():
         "BIAS_R1": rebalanced(8 * P, 7),
         "BIAS_R2": rebalanced(32 * P, 3),
         "BIAS_NEG": rebalanced(128 * P, 2),
+        # G2 endomorphisms (bls_w4.h): psi = (conj(x) cx, conj(y) cy) with cx = (0, PSI_CX1);
+        # psi^2 = (x PSI2_CX, y PSI2_CY), both in Fp
+        "PSI_CX1": limbs(mont(cx[1])),
+        "PSI_CY0": limbs(mont(cy[0])),
+        "PSI_CY1": limbs(mont(cy[1])),
+        "PSI2_CX": limbs(mont(psi2x[0])),
+        "PSI2_CY": limbs(mont(psi2y[0])),
     }
     out = []
     w = out.append
@@ -161,6 +178,11 @@ def main():
     w("// per-lane limbs of constants: K_<NAME>[j] = limb j")
     for name, l in consts.items():
         w("__constant__ uint32_t K_%s[16] = {%s};" % (name, ", ".join("0x%08xu" % v for v in l)))
+    w("// subtraction biases 2^k p (k = 1..10) for bls_w4.h, lower limbs pre-borrowed (2 units)")
+    w("__constant__ uint32_t K_BIASK[10][16] = {")
+    for kk in range(1, 11):
+        w("  {%s}," % ", ".join("0x%08xu" % v for v in rebalanced((1 << kk) * P, 2)))
+    w("};")
     w("}}  // namespace gbls::dfp")
     print("\n".join(out))
 
