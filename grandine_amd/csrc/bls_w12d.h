@@ -24,7 +24,8 @@ constexpr int WS = dfp::W12D_NSLOT * 16;
 struct Eng {
   dfp::Tabs t;
   uint32_t row, j;
-  uint32_t pre[2], r1[3], r2[2];  // packed plan bytes of this row
+  uint32_t pre[2], r1[3], r2[2];  // packed plan bytes of this row (product)
+  uint32_t sl[2], srp, srn, s1[3], s2[2];  // ... and of the squaring
   uint32_t *ws;                   // WS words of LDS
 };
 
@@ -51,6 +52,26 @@ __device__ __forceinline__ void begin(Eng &e, uint32_t *ws) {
   for (int k = 0; k < 5; k++) b[k] = r < 12 ? dfp::W12D_R2[r][k] : (uint32_t)dfp::W12D_ZERO;
   e.r2[0] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
   e.r2[1] = b[4];
+  // squaring plan (36 product rows)
+#pragma unroll
+  for (int k = 0; k < 8; k++) b[k] = r < 36 ? dfp::W12S_L[r][k] : 12u;
+  e.sl[0] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+  e.sl[1] = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+#pragma unroll
+  for (int k = 0; k < 4; k++) b[k] = r < 36 ? dfp::W12S_RP[r][k] : 12u;
+  e.srp = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+#pragma unroll
+  for (int k = 0; k < 4; k++) b[k] = r < 36 ? dfp::W12S_RN[r][k] : 12u;
+  e.srn = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+#pragma unroll
+  for (int k = 0; k < 12; k++) b[k] = r < 18 ? dfp::W12S_R1[r][k] : (uint32_t)dfp::W12D_ZERO;
+  e.s1[0] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+  e.s1[1] = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+  e.s1[2] = b[8] | b[9] << 8 | b[10] << 16 | b[11] << 24;
+#pragma unroll
+  for (int k = 0; k < 5; k++) b[k] = r < 12 ? dfp::W12S_R2[r][k] : (uint32_t)dfp::W12D_ZERO;
+  e.s2[0] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+  e.s2[1] = b[4];
   if (threadIdx.x < 16) ws[16 * dfp::W12D_ZERO + threadIdx.x] = 0;
   __syncthreads();
 }
@@ -91,6 +112,54 @@ __device__ __forceinline__ void mul(Eng &e, uint32_t *c, const uint32_t *a, cons
     for (int k = 0; k < 3; k++) s += e.ws[16 * byte_of(e.r2, k) + e.j];
 #pragma unroll
     for (int k = 3; k < 5; k++) s -= e.ws[16 * byte_of(e.r2, k) + e.j];
+    c[16 * e.row + e.j] = dfp::norm(s);
+  }
+  __syncthreads();
+}
+
+// c = a^2 (c may alias a): 36 row products (the three-level Karatsuba tree with Fp2
+// squarings (x0 + x1)(x0 - x1), x0 x1 at the leaves, tools/gen_wave12.py build_sqr), then the
+// product's R1 / R2 rounds with the squaring's plan.  All threads call it.
+__device__ __forceinline__ void sqr(Eng &e, uint32_t *c, const uint32_t *a) {
+  if (e.row < 36) {
+    const uint32_t *zero = e.ws + 16 * dfp::W12D_ZERO;
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t q = byte_of(e.sl, k);
+      x += (q == 12 ? zero : a + 16 * q)[e.j];
+    }
+    uint32_t y = dfp::konst(dfp::K_BIAS_SQ);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t q = (e.srp >> (8 * k)) & 0xffu;
+      y += (q == 12 ? zero : a + 16 * q)[e.j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t q = (e.srn >> (8 * k)) & 0xffu;
+      y -= (q == 12 ? zero : a + 16 * q)[e.j];
+    }
+    // x: <= 8 coefficients (< 1024 p); y: 1024 p + <= 4 - <= 4 coefficients (< 1536 p)
+    const uint32_t p = dfp::mul(dfp::norm(x), dfp::norm(y), e.t);
+    e.ws[16 * e.row + e.j] = p;
+  }
+  __syncthreads();
+  if (e.row < 18) {
+    uint32_t s = dfp::konst(dfp::K_BIAS_R1);
+#pragma unroll
+    for (int k = 0; k < 6; k++) s += e.ws[16 * byte_of(e.s1, k) + e.j];
+#pragma unroll
+    for (int k = 6; k < 12; k++) s -= e.ws[16 * byte_of(e.s1, k) + e.j];
+    e.ws[16 * (54 + e.row) + e.j] = dfp::norm(s);
+  }
+  __syncthreads();
+  if (e.row < 12) {
+    uint32_t s = dfp::konst(dfp::K_BIAS_R2);
+#pragma unroll
+    for (int k = 0; k < 3; k++) s += e.ws[16 * byte_of(e.s2, k) + e.j];
+#pragma unroll
+    for (int k = 3; k < 5; k++) s -= e.ws[16 * byte_of(e.s2, k) + e.j];
     c[16 * e.row + e.j] = dfp::norm(s);
   }
   __syncthreads();
@@ -137,7 +206,7 @@ __device__ __forceinline__ void frob2(Eng &e, uint32_t *c, const uint32_t *a) {
 __device__ __forceinline__ void exp_x(Eng &e, uint32_t *c, const uint32_t *a) {
   copy(e, c, a);
   for (int i = 62; i >= 0; i--) {
-    mul(e, c, c, c);
+    sqr(e, c, c);
     if ((dfp::X_ABS >> i) & 1) mul(e, c, c, a);
   }
   conj(e, c, c);

@@ -44,6 +44,12 @@ __device__ __forceinline__ void init(Ctx &c) {
   c.one = dfp::konst(dfp::K_ONE);
 }
 
+// A latency-chain kernel claims its SIMD: the clobbers make it allocate 256 VGPRs + 256 AGPRs
+// (occupancy 1), so no wave of a concurrent kernel (the signature / key side streams) is ever
+// co-resident and competes for its issue slots.  Used for launches of a few hundred waves.
+__device__ __forceinline__ void exclusive_simd() { asm volatile("" ::: "v255", "a255"); }
+constexpr uint32_t kExclusiveMaxWaves = 512;
+
 // ---- rows
 __device__ __forceinline__ uint32_t sel(const Ctx &c, uint32_t x0, uint32_t x1, uint32_t x2,
                                         uint32_t x3) {
@@ -567,6 +573,92 @@ __device__ __forceinline__ void line_add_aff(const Ctx &c, J &T, const A2 &Q, f2
   T.x = neg<2, 3>(c, kara(c, l0, l1, l2));
   T.y = sub<2, 3>(c, kara(c, y0, y1, y2), kara(c, k0, k1, k2));
   T.z = neg<2, 3>(c, kara(c, z0, z1, z2));
+}
+
+// Addition step T + Q for a homogeneous Q = (Xq, Yq, Zq) (T < 64 p, Q < 64 p): the general
+// add-1998-cmo-2 update and the line through T and Q scaled by Zq^2 (an Fp2 factor, which the
+// final exponentiation removes):
+//   th = Y1 Zq - Yq Z1, la = X1 Zq - Xq Z1;  L0 = th Xq - la Yq, L2 = -th Zq, L3 = la Zq;
+//   nv = la^3, R = la^2 X1 Zq, A = th^2 Z1 Zq + nv - 2R:
+//   X3 = -la A, Y3 = nv Y1 Zq - th (R - A), Z3 = -nv Z1 Zq.
+// 13 rounds; out T (< 4, < 8), (< 7, < 13), (< 4, < 8).
+__device__ __forceinline__ void line_add_proj(const Ctx &c, J &T, const J &Q, f2 &L0, f2 &L2,
+                                              f2 &L3) {
+  const uint32_t zqs = add(Q.z.c0, Q.z.c1), z1s = add(T.z.c0, T.z.c1);
+  // R1: Y1 Zq, Yq Z1 [0]
+  uint32_t a0, a1, a2, b0;
+  mul4(c, a0, a1, a2, b0, T.y.c0, Q.z.c0, T.y.c1, Q.z.c1, add(T.y.c0, T.y.c1), zqs, Q.y.c0, T.z.c0);
+  // R2: Yq Z1 [1, 2], X1 Zq [0, 1]
+  uint32_t b1, b2, e0, e1;
+  mul4(c, b1, b2, e0, e1, Q.y.c1, T.z.c1, add(Q.y.c0, Q.y.c1), z1s, T.x.c0, Q.z.c0, T.x.c1, Q.z.c1);
+  // R3: X1 Zq [2], Xq Z1
+  uint32_t e2, g0, g1, g2;
+  mul4(c, e2, g0, g1, g2, add(T.x.c0, T.x.c1), zqs, Q.x.c0, T.z.c0, Q.x.c1, T.z.c1,
+       add(Q.x.c0, Q.x.c1), z1s);
+  const f2 Y1Zq = kara(c, a0, a1, a2), X1Zq = kara(c, e0, e1, e2);
+  const f2 th = sub<2, 3>(c, Y1Zq, kara(c, b0, b1, b2));  // (< 7, < 13)
+  const f2 la = sub<2, 3>(c, X1Zq, kara(c, g0, g1, g2));
+  // R4: th^2, la^2
+  uint32_t u0, ux, v0, vx;
+  mul4(c, u0, ux, v0, vx, add(th.c0, th.c1), sub<4>(c, th.c0, th.c1), th.c0, th.c1,
+       add(la.c0, la.c1), sub<4>(c, la.c0, la.c1), la.c0, la.c1);
+  const f2 uu = sqr_of(u0, ux), vv = sqr_of(v0, vx);
+  const uint32_t ths = add(th.c0, th.c1), las = add(la.c0, la.c1);
+  // R5: th Xq, Z1 Zq [0]
+  uint32_t p0, p1, p2, z0;
+  mul4(c, p0, p1, p2, z0, th.c0, Q.x.c0, th.c1, Q.x.c1, ths, add(Q.x.c0, Q.x.c1), T.z.c0, Q.z.c0);
+  // R6: la Yq, Z1 Zq [1]
+  uint32_t q0, q1, q2, z1;
+  mul4(c, q0, q1, q2, z1, la.c0, Q.y.c0, la.c1, Q.y.c1, las, add(Q.y.c0, Q.y.c1), T.z.c1, Q.z.c1);
+  L0 = sub<2, 3>(c, kara(c, p0, p1, p2), kara(c, q0, q1, q2));
+  // R7: th Zq, Z1 Zq [2]
+  uint32_t r0, r1, r2, z2;
+  mul4(c, r0, r1, r2, z2, th.c0, Q.z.c0, th.c1, Q.z.c1, ths, zqs, z1s, zqs);
+  L2 = neg<2, 3>(c, kara(c, r0, r1, r2));
+  const f2 Z1Zq = kara(c, z0, z1, z2);
+  // R8: la Zq, nv = vv la [0]
+  uint32_t s0, s1, s2, n0;
+  mul4(c, s0, s1, s2, n0, la.c0, Q.z.c0, la.c1, Q.z.c1, las, zqs, vv.c0, la.c0);
+  L3 = kara(c, s0, s1, s2);
+  // R9: nv [1, 2], R = vv X1Zq [0, 1]
+  uint32_t n1, n2, w0, w1;
+  mul4(c, n1, n2, w0, w1, vv.c1, la.c1, add(vv.c0, vv.c1), las, vv.c0, X1Zq.c0, vv.c1, X1Zq.c1);
+  const f2 nv = kara(c, n0, n1, n2);
+  // R10: R [2], uu Z1Zq
+  uint32_t w2, m0, m1, m2;
+  mul4(c, w2, m0, m1, m2, add(vv.c0, vv.c1), add(X1Zq.c0, X1Zq.c1), uu.c0, Z1Zq.c0, uu.c1, Z1Zq.c1,
+       add(uu.c0, uu.c1), add(Z1Zq.c0, Z1Zq.c1));
+  const f2 R = kara(c, w0, w1, w2);
+  const f2 A = sub<3, 4>(c, add(kara(c, m0, m1, m2), nv), small(R, 2));  // (< 14, < 26)
+  const f2 rma = sub<5, 5>(c, R, A);
+  // R11: la A, nv Y1Zq [0]
+  uint32_t l0, l1, l2, y0;
+  mul4(c, l0, l1, l2, y0, la.c0, A.c0, la.c1, A.c1, las, add(A.c0, A.c1), nv.c0, Y1Zq.c0);
+  // R12: nv Y1Zq [1, 2], th (R - A) [0, 1]
+  uint32_t y1, y2, k0, k1;
+  mul4(c, y1, y2, k0, k1, nv.c1, Y1Zq.c1, add(nv.c0, nv.c1), add(Y1Zq.c0, Y1Zq.c1), th.c0, rma.c0,
+       th.c1, rma.c1);
+  // R13: th (R - A) [2], nv Z1Zq
+  uint32_t k2, x0, x1, x2;
+  mul4(c, k2, x0, x1, x2, ths, add(rma.c0, rma.c1), nv.c0, Z1Zq.c0, nv.c1, Z1Zq.c1,
+       add(nv.c0, nv.c1), add(Z1Zq.c0, Z1Zq.c1));
+  T.x = neg<2, 3>(c, kara(c, l0, l1, l2));
+  T.y = sub<2, 3>(c, kara(c, y0, y1, y2), kara(c, k0, k1, k2));
+  T.z = neg<2, 3>(c, kara(c, x0, x1, x2));
+}
+// Jacobian (X, Y, Z) -> homogeneous (X Z, Y, Z^3) of the same point (two rounds); out < 5 p
+__device__ __forceinline__ void jac_to_hom(const Ctx &c, J &o, const J &p) {
+  const uint32_t zs = add(p.z.c0, p.z.c1);
+  uint32_t s0, sx, m0, m1;
+  mul4(c, s0, sx, m0, m1, zs, sub<10>(c, p.z.c0, p.z.c1), p.z.c0, p.z.c1, p.x.c0, p.z.c0, p.x.c1,
+       p.z.c1);
+  const f2 Z2 = sqr_of(s0, sx);
+  uint32_t m2, t0, t1, t2;
+  mul4(c, m2, t0, t1, t2, add(p.x.c0, p.x.c1), zs, Z2.c0, p.z.c0, Z2.c1, p.z.c1,
+       add(Z2.c0, Z2.c1), zs);
+  o.x = kara(c, m0, m1, m2);
+  o.y = p.y;
+  o.z = kara(c, t0, t1, t2);
 }
 
 // x^(p-2) = (x^((p-3)/4))^4 x: the inverse of a nonzero x (every row, redundantly)

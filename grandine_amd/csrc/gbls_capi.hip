@@ -139,7 +139,7 @@ struct Ctx {
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
-  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, gpart, lines, Ts, V0, V1, tab, part, err, out0,
+  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, Sj, gpart, lines, Ts, V0, V1, tab, part, err, out0,
       out1, pks, pre, pre2, msm, sigd, sigst;
   // per-call option of the next pipeline_partials on this lease: compressed signatures
   // (96 B each, device) to decompress on the signature-side stream into `sigs`, with their
@@ -636,6 +636,13 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     return false;
   if (!c.upload_staged(c.tab, tab.data(), tab.size() * 4, st)) return false;
   const uint32_t N = (uint32_t)n, NP = (uint32_t)np, NS = (uint32_t)nseg;
+  // latency regime: each segment's S = sum r_i sig_i stays Jacobian (no inversion), its lines
+  // taken projectively (k_lines_w4j)
+  g2j *sj = nullptr;
+  if (!msm && !single && !sliced && X == 1 && nseg <= kW4Max) {
+    if (!c.ensure(c.Sj, nseg * sizeof(g2j) + 16)) return false;
+    sj = c.Sj.as<g2j>();
+  }
   const uint32_t *T = c.tab.as<uint32_t>();
   g2j *gpart = c.gpart.as<g2j>();
   int32_t *gpart_err = reinterpret_cast<int32_t *>(gpart + nchunks);
@@ -688,20 +695,26 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     else
       launch_g2sum(side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
                    T + segoff_at, NS, N, pks, rands, pre, pre2, empty_is_error, gpart, gpart_err,
-                   c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
+                   c.P.as<g1s>(), c.H.as<g2a>(), seg_err, sj);
   }
   {  // the extra pairs' lines of the first event slice (all events when not sliced)
     StageTimer t(S_LINES_S, side2);
-    launch_lines(side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, EC, c.Ts.as<g2h>(),
-                 c.lines.as<uint32_t>());
+    if (!sj || !launch_lines_jac(side2, sj, 1, N, NS, NP, c.lines.as<uint32_t>()))
+      launch_lines(side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, EC, c.Ts.as<g2h>(),
+                   c.lines.as<uint32_t>());
   }
+  // latency regime: H(m) stays Jacobian (over Q[2 i]) and its lines take it projectively,
+  // no inversion on the main chain
+  const bool jac_h = !sliced && N <= kW4Max;
   {
     StageTimer t(S_H2C_CLEAR, st);
-    launch_h2c_clear(st, c.Q.as<g2j>(), N, c.H.as<g2a>());
+    if (!jac_h || !launch_h2c_clear_jac(st, c.Q.as<g2j>(), N))
+      launch_h2c_clear(st, c.Q.as<g2j>(), N, c.H.as<g2a>());
   }
   {  // the sets' lines of the first event slice, before the join
     StageTimer t(S_LINES, st);
-    launch_lines(st, c.H.as<g2a>(), 0, N, NP, 0, EC, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
+    if (!jac_h || !launch_lines_jac(st, c.Q.as<g2j>(), 2, 0, N, NP, c.lines.as<uint32_t>()))
+      launch_lines(st, c.H.as<g2a>(), 0, N, NP, 0, EC, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
   }
   HIPCHK(hipEventRecord(c.ev_side1, side1));
   HIPCHK(hipEventRecord(c.ev_side2, side2));

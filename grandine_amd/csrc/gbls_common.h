@@ -61,6 +61,9 @@ void launch_h2c_field(hipStream_t st, const uint8_t *msg, const uint32_t *off, u
                       const uint8_t *dst, uint32_t dlen, fp2 *U);
 void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q);
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H);
+// the latency regime's pipeline form (n <= kW4Max, else false): the cleared points stay
+// Jacobian, written over Q[2 i]
+bool launch_h2c_clear_jac(hipStream_t st, g2j *Q, uint32_t n);
 
 // k_scalar.hip -- random-scalar products and the per-segment signature sum
 // P_i = r_i pk_i as line-evaluation points (bls_pairing.h g1s), quad per set
@@ -73,7 +76,7 @@ void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                   const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
                   int empty_is_error, g2j *part, int32_t *part_err, g1s *P, g2a *H,
-                  int32_t *seg_err);
+                  int32_t *seg_err, g2j *Sj = nullptr);
 // single checks (r = 1, one set per segment): the extra pair of segment s is (-g1, sig_s)
 void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
                      const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err);
@@ -104,6 +107,10 @@ void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
 // stored at event e - e0; Ts: the running point between event slices (null: full range)
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
                   int e0, int e1, g2h *Ts, uint32_t *lines);
+// all events of pairs [first, first + count) from Jacobian points Qj[stride i] (count <=
+// kW4Max, else false)
+bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t first, uint32_t count,
+                      uint32_t np, uint32_t *lines);
 
 // k_miller.hip -- Miller product tree + Horner
 // groups: (first index into plist, stride, count) per group, segment by segment

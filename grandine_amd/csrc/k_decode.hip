@@ -2,6 +2,7 @@
 // one lane per point.
 
 #include "gbls_common.h"
+#include "bls_w4.h"
 
 namespace gbls {
 
@@ -25,8 +26,10 @@ __global__ void __launch_bounds__(WG) k_g1_decompress(const uint8_t *in, uint32_
   st[i] = s;
 }
 
+template <bool X>
 __global__ void __launch_bounds__(WG) k_g2_decompress(const uint8_t *in, uint32_t n, g2a *out,
                                                       int32_t *st) {
+  if constexpr (X) w4::exclusive_simd();
   uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
   g2a a;
@@ -70,7 +73,9 @@ void launch_g1_decompress(hipStream_t st, const uint8_t *in, uint32_t n, int val
   if (n) k_g1_decompress<<<nblk(n), WG, 0, st>>>(in, n, validate, out, status);
 }
 void launch_g2_decompress(hipStream_t st, const uint8_t *in, uint32_t n, g2a *out, int32_t *status) {
-  if (n) k_g2_decompress<<<nblk(n), WG, 0, st>>>(in, n, out, status);
+  if (n)
+    (nblk(n) <= w4::kExclusiveMaxWaves ? k_g2_decompress<true> : k_g2_decompress<false>)<<<nblk(n), WG, 0, st>>>(
+        in, n, out, status);
 }
 void launch_g2_check(hipStream_t st, const g2a *in, uint32_t n, int32_t *status, int accumulate) {
   if (n) k_g2_check<<<nblk(n), WG, 0, st>>>(in, n, status, accumulate);

@@ -94,7 +94,9 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n,
 
 // one wave per message (bls_w4.h: four row-distributed products per round), the smallest
 // launches: Q0 + Q1, the cofactor clearing and the affine conversion at ~0.5 us per round
+template <bool X>
 __global__ void __launch_bounds__(64) k_h2c_clear_w4(const g2j *Q, uint32_t n, g2a *H) {
+  if constexpr (X) w4::exclusive_simd();
   const uint32_t i = blockIdx.x;
   if (i >= n) return;  // whole waves
   w4::Ctx c;
@@ -107,10 +109,32 @@ __global__ void __launch_bounds__(64) k_h2c_clear_w4(const g2j *Q, uint32_t n, g
   w4::store_affine(c, H + i, h);
 }
 
+// the pipeline's form: the cleared point stays Jacobian (no inversion: the Miller lines take
+// it projectively), written over Q[2 i]
+template <bool X>
+__global__ void __launch_bounds__(64) k_h2c_clear_w4j(g2j *Q, uint32_t n) {
+  if constexpr (X) w4::exclusive_simd();
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;  // whole waves
+  w4::Ctx c;
+  w4::init(c);
+  w4::J a, b, h;
+  w4::load(c, a, Q[2 * i]);
+  w4::load(c, b, Q[2 * i + 1]);
+  w4::add(c, a, a, b);
+  w4::clear_cofactor(c, h, a);
+  w4::store_jac(c, Q + 2 * i, h);
+}
+bool launch_h2c_clear_jac(hipStream_t st, g2j *Q, uint32_t n) {
+  if (!n || n > kW4Max) return false;
+  (n <= w4::kExclusiveMaxWaves ? k_h2c_clear_w4j<true> : k_h2c_clear_w4j<false>)<<<n, 64, 0, st>>>(Q, n);
+  return true;
+}
+
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   if (!n) return;
   if (n <= kW4Max)
-    k_h2c_clear_w4<<<n, 64, 0, st>>>(Q, n, H);
+    (n <= w4::kExclusiveMaxWaves ? k_h2c_clear_w4<true> : k_h2c_clear_w4<false>)<<<n, 64, 0, st>>>(Q, n, H);
   else if (n >= kLaneRegimeClear)
     k_h2c_clear_lane<<<nblk(n), WG, 0, st>>>(Q, n, H);
   else if (n <= g_row_clear_max)

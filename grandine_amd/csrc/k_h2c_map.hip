@@ -3,6 +3,7 @@
 // per field element for the SSWU map).  Output: affine points (Miller-loop input).
 #include "gbls_common.h"
 #include "bls_dfp.h"
+#include "bls_w4.h"
 
 namespace gbls {
 
@@ -26,7 +27,9 @@ struct RowPow {
     dfp::to_words_all(r.l, x, t);
   }
 };
+template <bool X>
 __global__ void __launch_bounds__(WG) k_h2c_map_row(const fp2 *U, uint32_t nu, g2j *Q) {
+  if constexpr (X) w4::exclusive_simd();
   const uint32_t i = (blockIdx.x * WG + threadIdx.x) >> 4;
   if (i >= nu) return;  // whole rows
   g2j q;
@@ -40,7 +43,8 @@ constexpr uint32_t kMapRowsMax = 2048;
 void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q) {
   if (!nu) return;
   if (nu <= kMapRowsMax)
-    k_h2c_map_row<<<nblk((size_t)nu * 16), WG, 0, st>>>(U, nu, Q);
+    (nblk((size_t)nu * 16) <= w4::kExclusiveMaxWaves ? k_h2c_map_row<true> : k_h2c_map_row<false>)<<<
+        nblk((size_t)nu * 16), WG, 0, st>>>(U, nu, Q);
   else
     k_h2c_map<<<nblk(nu), WG, 0, st>>>(U, nu, Q);
 }

@@ -1,6 +1,7 @@
 // gfx950 kernels: segmented point aggregation (a4, a5, a11: one 256-lane workgroup per
 // segment), key material for fixtures (a15) and the v_mad_u64_u32 roofline probe.
 #include "gbls_common.h"
+#include "bls_w4.h"
 
 namespace gbls {
 
@@ -149,10 +150,11 @@ __device__ __forceinline__ void jac_row_fold(jac<F> &acc, uint32_t &flag) {
   jac_add(acc, acc, o);  // lanes past the row end read zeros: infinity
 }
 // segment s = sum of pts[i] (idx == nullptr) or reg[idx[i]], i in [off[s], off[s+1])
-template <class F>
+template <class F, bool X>
 __global__ void __launch_bounds__(WG) k_aggregate_rows(const aff<F> *pts, uint32_t nreg,
                                                        const uint32_t *idx, const uint32_t *off,
                                                        uint32_t nseg, aff<F> *out, int32_t *st) {
+  if constexpr (X) w4::exclusive_simd();
   uint32_t t = blockIdx.x * WG + threadIdx.x;
   uint32_t s = t >> 4, r = t & 15;
   if (s >= nseg) return;  // whole rows
@@ -258,7 +260,7 @@ __global__ void __launch_bounds__(256) k_mad_peak(uint64_t *sink, uint32_t iters
 void launch_g1_aggregate_seg(hipStream_t st, const g1a *pks, const uint32_t *off, uint32_t nseg,
                              g1a *out, int32_t *status) {
   if (nseg >= kRowAggregateMinSegs)
-    k_aggregate_rows<fp><<<nblk(16 * (size_t)nseg), WG, 0, st>>>(pks, 0, nullptr, off, nseg, out,
+    (nblk(16 * (size_t)nseg) <= w4::kExclusiveMaxWaves ? k_aggregate_rows<fp, true> : k_aggregate_rows<fp, false>)<<<nblk(16 * (size_t)nseg), WG, 0, st>>>(pks, 0, nullptr, off, nseg, out,
                                                                  status);
   else if (nseg)
     k_g1_aggregate_seg<<<nseg, WGR, 0, st>>>(pks, off, nseg, out, status);
@@ -266,7 +268,7 @@ void launch_g1_aggregate_seg(hipStream_t st, const g1a *pks, const uint32_t *off
 void launch_g2_aggregate_seg(hipStream_t st, const g2a *pts, const uint32_t *off, uint32_t nseg,
                              g2a *out, int32_t *status) {
   if (nseg >= kRowAggregateMinSegs)
-    k_aggregate_rows<fp2><<<nblk(16 * (size_t)nseg), WG, 0, st>>>(pts, 0, nullptr, off, nseg, out,
+    (nblk(16 * (size_t)nseg) <= w4::kExclusiveMaxWaves ? k_aggregate_rows<fp2, true> : k_aggregate_rows<fp2, false>)<<<nblk(16 * (size_t)nseg), WG, 0, st>>>(pts, 0, nullptr, off, nseg, out,
                                                                   status);
   else if (nseg)
     k_g2_aggregate_seg<<<nseg, WGR, 0, st>>>(pts, off, nseg, out, status);
@@ -274,7 +276,7 @@ void launch_g2_aggregate_seg(hipStream_t st, const g2a *pts, const uint32_t *off
 void launch_g1_aggregate_idx(hipStream_t st, const g1a *reg, uint32_t nreg, const uint32_t *idx,
                              const uint32_t *off, uint32_t nseg, g1a *out, int32_t *status) {
   if (nseg >= kRowAggregateMinSegs)
-    k_aggregate_rows<fp><<<nblk(16 * (size_t)nseg), WG, 0, st>>>(reg, nreg, idx, off, nseg, out,
+    (nblk(16 * (size_t)nseg) <= w4::kExclusiveMaxWaves ? k_aggregate_rows<fp, true> : k_aggregate_rows<fp, false>)<<<nblk(16 * (size_t)nseg), WG, 0, st>>>(reg, nreg, idx, off, nseg, out,
                                                                  status);
   else if (nseg)
     k_g1_aggregate_idx<<<nseg, WGR, 0, st>>>(reg, nreg, idx, off, nseg, out, status);

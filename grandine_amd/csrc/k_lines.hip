@@ -127,8 +127,10 @@ __device__ __forceinline__ void line_put_w4(const w4::Ctx &c, uint32_t *L, uint3
   w = dfp::word_of(w4::sel(c, l3.c0, l3.c1, l3.c0, l3.c1), c.t);
   if (j < 12 && c.r < 2) L[line_word(e, 4 + (int)c.r, (int)j, np, pair)] = w;
 }
+template <bool X>
 __global__ void __launch_bounds__(64) k_lines_w4(const g2a *H, uint32_t first, uint32_t count,
                                                  uint32_t np, int e0, int e1, g2h *Ts, uint32_t *L) {
+  if constexpr (X) w4::exclusive_simd();
   const uint32_t i = blockIdx.x;
   if (i >= count) return;  // whole waves
   const uint32_t pair = first + i;
@@ -176,11 +178,54 @@ __global__ void __launch_bounds__(64) k_lines_w4(const g2a *H, uint32_t first, u
   }
 }
 
+// all 68 events of pairs [0, count) from Jacobian points Qj[stride i] (k_h2c_clear_w4j):
+// T starts as the homogeneous form of Q and the addition steps take Q projectively (lines
+// scaled by Fp2 factors, which the final exponentiation removes)
+template <bool X>
+__global__ void __launch_bounds__(64) k_lines_w4j(const g2j *Qj, uint32_t stride, uint32_t first,
+                                                  uint32_t count, uint32_t np, uint32_t *L) {
+  if constexpr (X) w4::exclusive_simd();
+  const uint32_t i = blockIdx.x, pair = first + i;
+  if (i >= count) return;  // whole waves
+  const uint32_t j = threadIdx.x & 15, r = (threadIdx.x >> 4) & 3;
+  w4::Ctx c;
+  w4::init(c);
+  w4::J q;
+  w4::load(c, q, Qj[(size_t)stride * i]);
+  if (w4::is_inf(c, q)) {  // identity lines: L0 = 1, L2 = L3 = 0
+    uint32_t one = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) one = j == (uint32_t)k ? k::ONE_M[k] : one;
+    for (int e = 0; e < ML_EVENTS; e++)
+      for (uint32_t cc = r; cc < 6; cc += 4)
+        if (j < 12) L[line_word(e, (int)cc, (int)j, np, pair)] = cc == 0 ? one : 0u;
+    return;
+  }
+  w4::jac_to_hom(c, q, q);
+  w4::J T = q;
+  for (int e = 0; e < ML_EVENTS; e++) {
+    w4::f2 l0, l2, l3;
+    if (ev_is_dbl(e))
+      w4::line_dbl(c, T, l0, l2, l3);
+    else
+      w4::line_add_proj(c, T, q, l0, l2, l3);
+    line_put_w4(c, L, np, pair, e, l0, l2, l3);
+  }
+}
+bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t first, uint32_t count,
+                      uint32_t np, uint32_t *lines) {
+  if (!count || count > kW4Max) return false;
+  (count <= w4::kExclusiveMaxWaves ? k_lines_w4j<true> : k_lines_w4j<false>)<<<count, 64, 0, st>>>(
+      Qj, stride, first, count, np, lines);
+  return true;
+}
+
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
                   int e0, int e1, g2h *Ts, uint32_t *lines) {
   if (!count) return;
   if (count <= kW4Max)
-    k_lines_w4<<<count, 64, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
+    (count <= w4::kExclusiveMaxWaves ? k_lines_w4<true> : k_lines_w4<false>)<<<count, 64, 0, st>>>(
+        H, first, count, np, e0, e1, Ts, lines);
   else if (count >= kLaneRegimeLines)
     k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
   else if (count <= kRowRegimeMax)

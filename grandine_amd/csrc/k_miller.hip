@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(w12d::THREADS) k_ml_horner_d(const fp12 *V, ui
   __syncthreads();
   w12d::copy(e, acc, ev);
   for (int k = 1; k < ML_EVENTS; k++) {
-    if (ev_is_dbl(k)) w12d::mul(e, acc, acc, acc);
+    if (ev_is_dbl(k)) w12d::sqr(e, acc, acc);
     w12d::mul(e, acc, acc, ev + k * w12d::IMG);
   }
   w12d::conj(e, acc, acc);

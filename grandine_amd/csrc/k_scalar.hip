@@ -13,8 +13,10 @@ namespace gbls {
 // P_i = r_i pk_i as a line-evaluation point (x, y, c) = (X Z, Y, Z^3) of the Jacobian
 // result (bls_pairing.h g1s): no inversion.  One DPP quad per set, MSB-first
 // double-and-add with quad doublings / additions (bls_gang.h); lane 0 stores.
+template <bool X>
 __global__ void __launch_bounds__(WG) k_mv_g1mul(const g1a *pks, const uint64_t *rands, uint32_t n,
                                                  g1s *P) {
+  if constexpr (X) w4::exclusive_simd();
   uint32_t u = blockIdx.x * WG + threadIdx.x;
   uint32_t i = u >> 2;
   int q = (int)(u & 3);
@@ -224,12 +226,15 @@ void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint
   if (n >= kLaneRegimeSets)
     k_mv_g1mul_lane<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
   else
-    k_mv_g1mul<<<nblk(4 * (size_t)n), WG, 0, st>>>(pks, rands, n, P);
+    (nblk(4 * (size_t)n) <= w4::kExclusiveMaxWaves ? k_mv_g1mul<true> : k_mv_g1mul<false>)<<<
+        nblk(4 * (size_t)n), WG, 0, st>>>(pks, rands, n, P);
 }
 // the same halves, one wave per (set, half) (bls_w4.h): a doubling is four rounds of four
 // row-distributed products, a mixed addition eight -- the latency regime
+template <bool X>
 __global__ void __launch_bounds__(64) k_mv_g2mul_w4(const g2a *sigs, const uint64_t *rands,
                                                     uint32_t n, g2j *R) {
+  if constexpr (X) w4::exclusive_simd();
   const uint32_t t = blockIdx.x;
   if (t >= 2 * n) return;  // whole waves
   const uint32_t i = t < n ? t : t - n;
@@ -270,11 +275,13 @@ __global__ void __launch_bounds__(64) k_mv_g2mul_w4(const g2a *sigs, const uint6
 // level 2 on one wave per segment (bls_w4.h): the segment's chunk partials in sequence, the
 // 2^32 shift of the high half (32 doublings) and the affine conversion, ~0.3 ms instead of the
 // quads' ~0.6 ms (their one-lane inversion dominates)
+template <bool X>
 __global__ void __launch_bounds__(64) k_g2sum_final_w4(const g2j *part, const int32_t *part_err,
                                                        const uint32_t *chunks, const uint32_t *seg_chunk,
                                                        const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                                                        int empty_is_error, g1s *P, g2a *H,
-                                                       int32_t *seg_err) {
+                                                       int32_t *seg_err, g2j *Sj) {
+  if constexpr (X) w4::exclusive_simd();
   const uint32_t s = blockIdx.x;
   if (s >= nseg) return;
   w4::Ctx c;
@@ -295,7 +302,10 @@ __global__ void __launch_bounds__(64) k_g2sum_final_w4(const g2j *part, const in
   if (empty_is_error && seg_off[s + 1] == seg_off[s]) err = 1;
   for (int d = 0; d < 32; d++) w4::dbl(c, hi, hi);
   w4::add(c, lo, lo, hi);
-  w4::store_affine(c, H + n + s, lo);
+  if (Sj)
+    w4::store_jac(c, Sj + s, lo);  // the lines take it projectively (k_lines_w4j)
+  else
+    w4::store_affine(c, H + n + s, lo);
   if (threadIdx.x == 0) {
     g1s ng1;
     fp_set(ng1.x, k::G1X_M);
@@ -309,7 +319,8 @@ __global__ void __launch_bounds__(64) k_g2sum_final_w4(const g2j *part, const in
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R) {
   if (!n) return;
   if (2 * n <= kW4Max)
-    k_mv_g2mul_w4<<<2 * n, 64, 0, st>>>(sigs, rands, n, R);
+    (2 * n <= w4::kExclusiveMaxWaves ? k_mv_g2mul_w4<true> : k_mv_g2mul_w4<false>)<<<2 * n, 64, 0, st>>>(
+        sigs, rands, n, R);
   else
     k_mv_g2mul<<<nblk(8 * (size_t)n), WG, 0, st>>>(sigs, rands, n, R);
 }
@@ -317,12 +328,13 @@ void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                   const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
                   int empty_is_error, g2j *part, int32_t *part_err, g1s *P, g2a *H,
-                  int32_t *seg_err) {
+                  int32_t *seg_err, g2j *Sj) {
   if (nchunks)
     k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, rands, pre, pre2, part, part_err);
   if (nseg && nseg <= kW4Max)
-    k_g2sum_final_w4<<<nseg, 64, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n,
-                                          empty_is_error, P, H, seg_err);
+    (nseg <= w4::kExclusiveMaxWaves ? k_g2sum_final_w4<true> : k_g2sum_final_w4<false>)<<<nseg, 64, 0, st>>>(
+        part, part_err, chunks, seg_chunk, seg_off, nseg, n,
+                                          empty_is_error, P, H, seg_err, Sj);
   else if (nseg)
     k_g2sum_final<<<nseg, WG, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n,
                                        empty_is_error, P, H, seg_err);

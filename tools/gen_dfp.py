@@ -77,6 +77,46 @@ def w12d_plan():
     return plan_pre, plan_r1, plan_r2
 
 
+def w12d_sqr_plan():
+    """Per-row plan of the row-distributed Fp12 SQUARING (bls_w12d.h sqr): 36 products
+    (sum of lhs) * (bias + sum of rhs_pos - sum of rhs_neg) of tools/gen_wave12.py build_sqr,
+    then R1 (18 values, <= 6 + 6 product terms) and R2 (12 values, <= 3 + 2 R1 terms) in the
+    multiply plan's slot space: [0, 36) products, [54, 72) R1 values, 72 the zero slot."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import gen_wave12
+    lhs, rp, rn, post1, post2, post3 = gen_wave12.build_sqr()
+    n = len(lhs)
+    expr = {i: {i: 1} for i in range(n)}
+
+    def comb(terms):
+        r = {}
+        for src, g in terms:
+            for k, v in expr[src].items():
+                r[k] = r.get(k, 0) + g * v
+        return {k: v for k, v in r.items() if v}
+    for l, t in enumerate(post1):
+        expr[n + l] = comb(t)
+    r1 = [comb(t) for t in post2]
+    ZERO = 72
+    plan_l = [x + [12] * (8 - len(x)) for x in lhs]
+    plan_rp = [x + [12] * (4 - len(x)) for x in rp]
+    plan_rn = [x + [12] * (4 - len(x)) for x in rn]
+    plan_r1 = []
+    for o in r1:
+        pos = sorted(k for k, v in o.items() if v > 0 for _ in range(v))
+        neg = sorted(k for k, v in o.items() if v < 0 for _ in range(-v))
+        assert len(pos) <= 6 and len(neg) <= 6
+        plan_r1.append(pos + [ZERO] * (6 - len(pos)) + neg + [ZERO] * (6 - len(neg)))
+    plan_r2 = []
+    base2 = 2 * n
+    for t in post3:
+        pos = [54 + (src - base2) for src, g in t if g > 0]
+        neg = [54 + (src - base2) for src, g in t if g < 0]
+        assert all(base2 <= src < base2 + 18 for src, _ in t) and len(pos) <= 3 and len(neg) <= 2
+        plan_r2.append(pos + [ZERO] * (3 - len(pos)) + neg + [ZERO] * (2 - len(neg)))
+    return plan_l, plan_rp, plan_rn, plan_r1, plan_r2
+
+
 def mont(x):
     return x * R % P
 
@@ -124,6 +164,9 @@ def main():
         "BIAS_R1": rebalanced(8 * P, 7),
         "BIAS_R2": rebalanced(32 * P, 3),
         "BIAS_NEG": rebalanced(128 * P, 2),
+        # the squaring's (x0 - x1) operands subtract <= 4 coefficients (< 128 p each, limbs
+        # < 2^28 + 2^9): 1024 p with 5 units borrowed per limb
+        "BIAS_SQ": rebalanced(1024 * P, 5),
         # G2 endomorphisms (bls_w4.h): psi = (conj(x) cx, conj(y) cy) with cx = (0, PSI_CX1);
         # psi^2 = (x PSI2_CX, y PSI2_CY), both in Fp
         "PSI_CX1": limbs(mont(cx[1])),
@@ -156,6 +199,28 @@ def main():
     w("// R2: 3 positive then 2 negative R1 slots")
     w("__constant__ uint8_t W12D_R2[12][5] = {")
     for row in r2:
+        w("  {%s}," % ", ".join(str(v) for v in row))
+    w("};")
+    sl, srp, srn, sr1, sr2 = w12d_sqr_plan()
+    w("// Row-distributed Fp12 squaring (bls_w12d.h sqr): lhs / rhs+ / rhs- coefficient sets, R1, R2")
+    w("__constant__ uint8_t W12S_L[36][8] = {")
+    for row in sl:
+        w("  {%s}," % ", ".join(str(v) for v in row))
+    w("};")
+    w("__constant__ uint8_t W12S_RP[36][4] = {")
+    for row in srp:
+        w("  {%s}," % ", ".join(str(v) for v in row))
+    w("};")
+    w("__constant__ uint8_t W12S_RN[36][4] = {")
+    for row in srn:
+        w("  {%s}," % ", ".join(str(v) for v in row))
+    w("};")
+    w("__constant__ uint8_t W12S_R1[18][12] = {")
+    for row in sr1:
+        w("  {%s}," % ", ".join(str(v) for v in row))
+    w("};")
+    w("__constant__ uint8_t W12S_R2[12][5] = {")
+    for row in sr2:
         w("  {%s}," % ", ".join(str(v) for v in row))
     w("};")
     w("// Frobenius constants by exponent e of w: FROB1[e] = (c0, c1) of xi^(e (p - 1) / 6),")

@@ -109,6 +109,51 @@ def build():
     return prod, post1, post2, post3
 
 
+def build_sqr():
+    """The squaring plan: the same three-level Karatsuba tree applied to a*a, where every leaf
+    is an Fp2 SQUARING (x0 + x1)(x0 - x1), x0 x1 -- 36 Fp products instead of 54.  Returns
+    (lhs, rhs_pos, rhs_neg, post1, post2, post3): product l is (sum of lhs[l]) * (sum of
+    rhs_pos[l] - sum of rhs_neg[l]); the POST rounds as in build(), over [p_0..p_35 | POST1 |
+    POST2] (POST1 outputs: c0 = p0, c1 = 2 p1)."""
+    fp6_sets = {0: [0], 1: [1], 2: [0, 1]}
+    fp2_sets = {0: [0], 1: [1], 2: [2], 3: [1, 2], 4: [0, 1], 5: [0, 2]}
+    lhs, rp, rn = [], [], []
+    pid = {}
+    for i6 in range(3):
+        for j in range(6):
+            s0 = sorted(idx(h, jj, 0) for h in fp6_sets[i6] for jj in fp2_sets[j])
+            s1 = sorted(idx(h, jj, 1) for h in fp6_sets[i6] for jj in fp2_sets[j])
+            pid[(i6, j, 0)] = len(lhs)  # (x0 + x1)(x0 - x1)
+            lhs.append(sorted(s0 + s1))
+            rp.append(s0)
+            rn.append(s1)
+            pid[(i6, j, 1)] = len(lhs)  # x0 x1
+            lhs.append(s0)
+            rp.append(s1)
+            rn.append([])
+    assert len(lhs) == 36 and max(len(x) for x in lhs) == 8 and max(len(x) for x in rp + rn) == 4
+    post1 = []
+    v1 = {}
+    base1 = 36
+    for i6 in range(3):
+        for j in range(6):
+            v1[(i6, j, 0)] = base1 + len(post1)
+            post1.append([(pid[(i6, j, 0)], 1)])
+            v1[(i6, j, 1)] = base1 + len(post1)
+            post1.append([(pid[(i6, j, 1)], 1), (pid[(i6, j, 1)], 1)])
+    # POST2 / POST3: build()'s, with the POST1 value indices of this plan
+    _, p1ref, p2ref, p3ref = build()
+    remap = {}
+    for i6 in range(3):
+        for j in range(6):
+            for k in range(2):
+                remap[54 + 2 * (6 * i6 + j) + k] = v1[(i6, j, k)]
+    base2 = base1 + 36
+    post2 = [[(remap[src], g) for src, g in t] for t in p2ref]
+    post3 = [[(base2 + (src - 90), g) for src, g in t] for t in p3ref]
+    return lhs, rp, rn, post1, post2, post3
+
+
 def main():
     prod, post1, post2, post3 = build()
     base1, base2 = 54, 90

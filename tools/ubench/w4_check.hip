@@ -38,7 +38,7 @@ __device__ void store_j(const w4::Ctx &c, g2j *o, const w4::J &p) {
 
 // failure bits per wave: 1 gather, 2 dbl, 4 add, 8 add(P,P), 16 add(P,-P), 32 add(inf,Q),
 // 64 psi, 128 psi2, 256 [|x|]P, 512 clear, 1024 affine of clear, 2048 line_dbl, 4096 line_add,
-// 8192 madd, 16384 32-bit scalar chain
+// 8192 madd, 16384 32-bit scalar chain, 32768 projective addition step
 __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *fails) {
   w4::Ctx c;
   w4::init(c);
@@ -181,6 +181,45 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
     store_j(c, &out, acc);
     mul_u64(R, qa, k);
     if (!same(R)) f |= 16384;
+  }
+  // projective addition step: Q Jacobian -> homogeneous, T from a doubling of Q; the same point
+  // and proportional lines as the affine step (the lines carry an Fp2 factor)
+  {
+    g2a qa;
+    jac_to_aff(qa, Q);
+    g2h T;
+    T.x = qa.x;
+    T.y = qa.y;
+    fp2_one(T.z);
+    fp2 L0, L2, L3;
+    line_dbl(T, L0, L2, L3);
+    w4::J qh, jt;
+    w4::jac_to_hom(c, qh, jq);
+    {
+      g2j tj;
+      tj.x = T.x;
+      tj.y = T.y;
+      tj.z = T.z;
+      w4::load(c, jt, tj);
+    }
+    line_add_aff(T, qa, L0, L2, L3);
+    w4::f2 l0, l2, l3;
+    w4::line_add_proj(c, jt, qh, l0, l2, l3);
+    __shared__ fp2 ll[3];
+    __shared__ g2j tt;
+    w4::store4(c, l0.c0, l0.c1, l2.c0, l2.c1, ll[0].c0.l, ll[0].c1.l, ll[1].c0.l, ll[1].c1.l);
+    w4::store4(c, l3.c0, l3.c1, l3.c0, l3.c1, ll[2].c0.l, ll[2].c1.l, ll[2].c0.l, ll[2].c1.l);
+    store_j(c, &tt, jt);
+    __syncthreads();
+    fp2 a, b;
+    bool ok = true;
+    // same homogeneous point: X Z' = X' Z, Y Z' = Y' Z
+    fp2_mul(a, tt.x, T.z); fp2_mul(b, T.x, tt.z); ok &= fp2_eq(a, b);
+    fp2_mul(a, tt.y, T.z); fp2_mul(b, T.y, tt.z); ok &= fp2_eq(a, b);
+    // proportional lines: l0 L2 = L0 l2, l3 L2 = L3 l2
+    fp2_mul(a, ll[0], L2); fp2_mul(b, L0, ll[1]); ok &= fp2_eq(a, b);
+    fp2_mul(a, ll[2], L2); fp2_mul(b, L3, ll[1]); ok &= fp2_eq(a, b);
+    if (!ok) f |= 32768;
   }
   if (threadIdx.x == 0) fails[blockIdx.x] = f;
 }
