@@ -89,9 +89,9 @@ def cpu_threads():
 
 def pmc_traffic(kernel, default_cmd):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
-    summary of the default command (profiles/r02/pmc_bytes.csv, tools/prof/pmc_bytes.py;
+    summary of the default command (profiles/r03/pmc_bytes.csv, tools/prof/pmc_bytes.py;
     FETCH_SIZE doubled per the gfx950 correction).  None for other commands or if absent."""
-    path = os.path.join(ROOT, "profiles", "r02", "pmc_bytes.csv")
+    path = os.path.join(ROOT, "profiles", "r03", "pmc_bytes.csv")
     if not default_cmd or not os.path.exists(path):
         return None
     with open(path) as f:

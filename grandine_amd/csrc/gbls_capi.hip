@@ -405,6 +405,15 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
       g.devs.back()->ncu = prop.multiProcessorCount;
     }
   }
+  // direct xGMI peer access between the engine's devices (partials gathered device-to-device,
+  // registry replicas); without it hipMemcpyPeerAsync still works, staged by the runtime
+  for (int a : ids)
+    for (int b : ids) {
+      int can = 0;
+      if (a != b && hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can && hipSetDevice(a) == hipSuccess)
+        (void)hipDeviceEnablePeerAccess(b, 0);  // "already enabled" is fine
+    }
+  (void)hipGetLastError();
   g.ready.store(true);
   return true;
 }
@@ -801,11 +810,13 @@ bool upload_pks(Ctx &c, const PkSource &host, size_t b, size_t e, hipStream_t st
 
 // One device: host batch [sets b..e) in segments seg (rebased, host) -> per-segment
 // verdicts (host) when `verdicts`, or else the Miller partial + error flag of the single
-// segment into part_host / err_host.  Enqueues only; the caller synchronises `c.own`.
+// segment, copied device-to-device (hipMemcpyPeerAsync, xGMI) to part_dst / err_dst on
+// device dst_dev.  Enqueues only; the caller synchronises `c.own` (or waits on it).
 bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
                         const uint8_t *sigs_c, int32_t *sig_status, const PkSource &src,
                         const uint64_t *rands, size_t b, size_t e, const uint32_t *seg,
-                        size_t nseg, int32_t *verdicts, void *part_host, int32_t *err_host) {
+                        size_t nseg, int32_t *verdicts, fp12 *part_dst, int32_t *err_dst,
+                        int dst_dev) {
   hipStream_t st = c.own;
   size_t n = e - b;
   if (!c.begin(st)) return false;
@@ -845,8 +856,8 @@ bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
   if (verdicts) {
     HIPCHK(hipMemcpyAsync(verdicts, c.out1.p, nseg * 4, hipMemcpyDeviceToHost, st));
   } else {
-    HIPCHK(hipMemcpyAsync(part_host, c.part.p, sizeof(fp12), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(err_host, c.err.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyPeerAsync(part_dst, dst_dev, c.part.p, d.hipdev, sizeof(fp12), st));
+    HIPCHK(hipMemcpyPeerAsync(err_dst, dst_dev, c.err.p, d.hipdev, 4, st));
   }
   if (sigs_c) HIPCHK(hipMemcpyAsync(sig_status + b, c.sigst.p, n * 4, hipMemcpyDeviceToHost, st));
   return true;
@@ -860,12 +871,20 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
                  size_t nseg, int32_t *verdicts, int cls = 0) {
   std::shared_lock<std::shared_mutex> rl(g.reg_mu);
   const size_t ndev = g.devs.size();
-  // ---- one large batch: per-device Miller partials, one final exponentiation
+  // ---- one large batch: per-device Miller partials, gathered device-to-device onto device 0
+  // (hipMemcpyPeerAsync over xGMI, ordered by events, no host round trip), one final
+  // exponentiation there
   if (nseg == 1 && ndev > 1 && n >= 2 * kShardMinSets) {
     size_t k = std::min(ndev, n / kShardMinSets);
+    Device &d0 = *g.devs[0];
+    Lease L0(d0, cls);
+    if (!L0.ok() || !L0->begin(L0->own)) return false;
+    hipStream_t st0 = L0->own;
+    if (!L0->ensure(L0->part, k * sizeof(fp12)) || !L0->ensure(L0->err, k * 4 + 16) ||
+        !L0->ensure(L0->out1, 16))
+      return false;
     std::vector<std::unique_ptr<Lease>> leases;
-    std::vector<fp12> parts(k);
-    std::vector<int32_t> errs(k, 1);
+    std::vector<hipEvent_t> evs;
     bool ok = true;
     for (size_t j = 0; j < k && ok; j++) {
       size_t b = n * j / k, e = n * (j + 1) / k;
@@ -874,24 +893,31 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
       Lease &L = *leases.back();
       uint32_t seg[2] = {0, (uint32_t)(e - b)};
       ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, sigs_c, sig_status, src, rands, b, e,
-                                        seg, 1, nullptr, &parts[j], &errs[j]);
+                                        seg, 1, nullptr, L0->part.as<fp12>() + j,
+                                        L0->err.as<int32_t>() + j, d0.hipdev);
+      if (!ok) break;
+      hipEvent_t ev;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        ok = fail(GBLS_ERR_HIP);
+        break;
+      }
+      evs.push_back(ev);
+      if (hipEventRecord(ev, L->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
     }
-    for (auto &L : leases)
-      if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
-    leases.clear();
-    if (!ok) return false;
-    Device &d0 = *g.devs[0];
-    Lease L(d0, cls);
-    if (!L.ok() || !L->begin(L->own)) return false;
-    hipStream_t st = L->own;
-    if (!L->upload_staged(L->in0, parts.data(), k * sizeof(fp12), st) ||
-        !L->upload_staged(L->in1, errs.data(), k * 4, st) || !L->ensure(L->out1, 16))
-      return false;
-    if (!pipeline_final(L->in0.as<fp12>(), L->in1.as<int32_t>(), k, 1, L->out1.as<int32_t>(), st))
-      return false;
-    HIPCHK(hipMemcpyAsync(verdicts, L->out1.p, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return true;
+    if (ok && hipSetDevice(d0.hipdev) != hipSuccess) ok = fail(GBLS_ERR_HIP);
+    for (size_t j = 0; ok && j < evs.size(); j++)
+      if (hipStreamWaitEvent(st0, evs[j], 0) != hipSuccess) ok = fail(GBLS_ERR_HIP);
+    ok = ok && pipeline_final(L0->part.as<fp12>(), L0->err.as<int32_t>(), k, 1,
+                              L0->out1.as<int32_t>(), st0);
+    if (ok && hipMemcpyAsync(verdicts, L0->out1.p, 4, hipMemcpyDeviceToHost, st0) != hipSuccess)
+      ok = fail(GBLS_ERR_HIP);
+    // the final's stream waited on every shard, so its completion covers theirs (including the
+    // shards' signature-status copies to the host); on a failure every shard is drained
+    if (ok && hipStreamSynchronize(st0) != hipSuccess) ok = fail(GBLS_ERR_HIP);
+    if (!ok)
+      for (auto &L : leases) (void)hipStreamSynchronize((*L)->own);
+    for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+    return ok;
   }
   // ---- whole segments per device, contiguous groups balanced by set count
   size_t k = 1;
@@ -916,7 +942,7 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
     leases.emplace_back(new Lease(d, cls));
     Lease &L = *leases.back();
     ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, sigs_c, sig_status, src, rands, b, e,
-                                      segs[j].data(), s1 - s0, verdicts + s0, nullptr, nullptr);
+                                      segs[j].data(), s1 - s0, verdicts + s0, nullptr, nullptr, 0);
   }
   for (auto &L : leases)
     if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);

@@ -25,7 +25,10 @@ constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
 constexpr uint32_t kRowRegimeMax = 6144;
 // ... and the smallest launches run one wave per point (bls_w4.h): cofactor clearing and
 // Miller lines of up to this many points
-constexpr uint32_t kW4Max = 1024;
+#ifndef GBLS_W4_MAX
+#define GBLS_W4_MAX 1024
+#endif
+constexpr uint32_t kW4Max = GBLS_W4_MAX;
 constexpr uint32_t kRowClearMax = 4096;  // cofactor clearing on rows (up to one C2 batch)
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
 extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic (GBLS_ML_R28)

@@ -160,7 +160,12 @@ __global__ void __launch_bounds__(WGR) k_msm_scatter(const g2a *sigs, const uint
 __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_t *list,
                                                   const uint32_t *start, const uint32_t *cstart,
                                                   uint32_t nb, uint32_t max_chunks, g2j *chunk) {
-  __shared__ g2j xs[WG];
+  // structure-of-arrays image of the wave's partials: word w of lane l at xs[w * WG + l], so a
+  // wave's 64 lanes touch 64 consecutive words (distinct banks) on every store and load (the
+  // array-of-structures image, 288-byte stride, put 16 lanes on each bank: 80 % of the LDS
+  // cycles were conflicts)
+  constexpr int NW = sizeof(g2j) / 4;
+  __shared__ uint32_t xs[NW * WG];
   const uint32_t lane = threadIdx.x, base = blockIdx.x * WG;
   const uint32_t j = base + lane, total = cstart[nb];
   const bool live = j < max_chunks && j < total;
@@ -192,10 +197,15 @@ __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_
   uint32_t run = end - first;  // wave maximum of the run lengths
   for (int o = 32; o >= 1; o >>= 1) run = max(run, (uint32_t)__shfl_xor((int)run, o));
   for (uint32_t st = 1; st < run; st <<= 1) {
-    xs[lane] = acc;
+    const uint32_t *aw = reinterpret_cast<const uint32_t *>(&acc);
+#pragma unroll
+    for (int w = 0; w < NW; w++) xs[w * WG + lane] = aw[w];
     __syncthreads();
     if ((k & (2 * st - 1)) == 0 && lane + st < end) {
-      g2j x = xs[lane + st];
+      g2j x;
+      uint32_t *xw = reinterpret_cast<uint32_t *>(&x);
+#pragma unroll
+      for (int w = 0; w < NW; w++) xw[w] = xs[w * WG + lane + st];
       jac_add(acc, acc, x);
     }
     __syncthreads();

@@ -1,0 +1,46 @@
+"""The N-rank flow as fresh child processes: torch.distributed.run with 2
+ranks on the one GPU of the box (gloo, GBLS_BENCH_ONE_DEVICE), each started before it touches
+the GPU.  (1) tests/dist_flow.py: per-rank GPU partials, all-gather, final exponentiation on
+every rank; clean batch accepted, a corrupted shard rejected by every rank.  (2) bench.py's
+own 2-rank C2 leg (2 batches of 4096 sets per rank, all verdicts checked by the bench)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(args, timeout):
+    env = dict(os.environ, GBLS_BENCH_ONE_DEVICE="1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=%d" % _port()] + args
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_two_rank_partials_flow_rejects_corrupt_shard():
+    r = _run([os.path.join(ROOT, "tests", "dist_flow.py")], 300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["world"] == 2
+    for x in res["ranks"]:
+        assert x["clean"] == 0 and x["corrupt"] == 5, res
+
+
+def test_bench_two_rank_c2_leg():
+    r = _run([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu",
+              "--batches", "2"], 400)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0, line
