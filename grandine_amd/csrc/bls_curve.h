@@ -439,8 +439,51 @@ HD int32_t g1_decompress(g1a &r, const uint8_t *in) {
   if (fp_is_zero(x)) return ST_NOT_IN_GROUP;  // (0, +-2) has order 3
   return ST_SUCCESS;
 }
+// fp2_sqrt (bls_field.h) with the (p-3)/4 exponentiation as a policy, so that the latency
+// regime can run its two exponentiations row-distributed (bls_dfp.h, k_g2_decompress_row)
+template <class Pow>
+HD bool fp2_sqrt_pow(fp2 &r, const fp2 &a, const Pow &pow) {
+  if (fp2_is_zero(a)) {
+    fp2_zero(r);
+    return true;
+  }
+  fp n, t, gamma, g2;
+  fp_sqr(n, a.c0);
+  fp_sqr(t, a.c1);
+  fp_add(n, n, t);
+  pow(gamma, n);
+  fp_mul(gamma, gamma, n);  // n^((p+1)/4)
+  fp_sqr(g2, gamma);
+  if (!fp_eq(g2, n)) return false;
+  fp delta, x0, x0sq, tmp;
+  fp_add(delta, a.c0, gamma);
+  fp_half(delta, delta);
+  if (fp_is_zero(delta)) {  // only when a1 == 0 and gamma == -a0
+    fp_sub(delta, a.c0, gamma);
+    fp_half(delta, delta);
+  }
+  pow(t, delta);
+  fp_mul(x0, delta, t);
+  fp_sqr(x0sq, x0);
+  fp half_a1t;
+  fp_mul(tmp, a.c1, t);
+  fp_half(half_a1t, tmp);
+  const bool sq = fp_eq(x0sq, delta);
+  fp nh;
+  fp_neg(nh, half_a1t);
+  fp_sel(r.c0, sq, nh, x0);
+  fp_sel(r.c1, sq, x0, half_a1t);
+  fp2 chk;
+  fp2_sqr(chk, r);
+  return fp2_eq(chk, a);
+}
+struct LanePowCurve {
+  HD void operator()(fp &r, const fp &a) const { fp_pow_pm3d4(r, a); }
+};
+
 // blst POINTonE2_Uncompress_Z semantics (on-curve check only)
-HD int32_t g2_decompress(g2a &r, const uint8_t *in) {
+template <class Pow>
+HD int32_t g2_decompress_pow(g2a &r, const uint8_t *in, const Pow &pow) {
   f_zero(r.x);
   f_zero(r.y);
   uint8_t b0 = in[0];
@@ -461,12 +504,13 @@ HD int32_t g2_decompress(g2a &r, const uint8_t *in) {
   fp2_sqr(rhs, x);
   fp2_mul(rhs, rhs, x);
   fp2_add(rhs, rhs, fp2_const(k::B2_C0, k::B2_C1));
-  if (!fp2_sqrt(y, rhs)) return ST_NOT_ON_CURVE;
+  if (!fp2_sqrt_pow(y, rhs, pow)) return ST_NOT_ON_CURVE;
   if (fp2_lex_largest(y) != (bool)(b0 & 0x20)) fp2_neg(y, y);
   r.x = x;
   r.y = y;
   return ST_SUCCESS;
 }
+HD int32_t g2_decompress(g2a &r, const uint8_t *in) { return g2_decompress_pow(r, in, LanePowCurve()); }
 HD void g1_compress(uint8_t *out, const g1a &a) {
   if (aff_is_inf(a)) {
     out[0] = 0xc0;

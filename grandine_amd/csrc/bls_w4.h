@@ -661,6 +661,69 @@ __device__ __forceinline__ void jac_to_hom(const Ctx &c, J &o, const J &p) {
   o.z = kara(c, t0, t1, t2);
 }
 
+// ---- G1 (E: y^2 = x^3 + 4 over Fp) on the same rows: the random-scalar products r pk of the
+// latency regime.  Jacobian over Fp; out bounds in units of p.
+struct J1 {
+  uint32_t x, y, z;
+};
+// dbl-2009-l, inputs < 600 p: 3 rounds; out X < 33.001, Y < 17.001, Z < 2.0002.  o may alias p.
+__device__ __forceinline__ void dbl1(const Ctx &c, J1 &o, const J1 &p) {
+  uint32_t A, B, yz, d;
+  mul4(c, A, B, yz, d, p.x, p.x, p.y, p.y, p.y, p.z, p.x, p.x);
+  const uint32_t E = small(A, 3), t = add(p.x, B);
+  uint32_t C, T2, F;
+  mul4(c, C, T2, F, d, B, B, t, t, E, E, E, E);
+  const uint32_t D = small(sub<2>(c, T2, add(A, C)), 2);  // < 10.001
+  const uint32_t X3 = sub<5>(c, F, small(D, 2));           // < 33.001
+  const uint32_t u = sub<6>(c, D, X3);                     // < 74.002
+  uint32_t eu, d1, d2;
+  mul4(c, eu, d, d1, d2, E, u, E, u, E, u, E, u);
+  o.x = X3;
+  o.y = sub<4>(c, eu, small(C, 8));  // < 17.001
+  o.z = small(yz, 2);                // < 2.0002
+}
+// madd-2007-bl, r = a + (x2, y2) (affine, not infinity), a.x < 120 p, a.y < 60 p (dbl1 / madd1
+// outputs): 5 rounds + a zero test, jac_add_aff's cases; out X < 5.0004, Y < 5.0002, Z < 5.0003
+__device__ __forceinline__ void madd1(const Ctx &c, J1 &o, const J1 &a, uint32_t x2, uint32_t y2) {
+  uint32_t zz, yz, d, d1;
+  mul4(c, zz, yz, d, d1, a.z, a.z, y2, a.z, a.z, a.z, a.z, a.z);
+  uint32_t U2, S2;
+  mul4(c, U2, S2, d, d1, x2, zz, yz, zz, x2, zz, x2, zz);
+  const uint32_t H = sub<7>(c, U2, a.x);              // < 129
+  const uint32_t rr = small(sub<6>(c, S2, a.y), 2);   // < 130
+  const uint32_t zf = zero4(c, H, rr, a.z, a.z);
+  if ((zf & 0xc) == 0xc) {  // a = inf
+    o.x = x2;
+    o.y = y2;
+    o.z = c.one;
+    return;
+  }
+  if (zf & 1) {
+    if (zf & 2) {
+      J1 bj{x2, y2, c.one};
+      dbl1(c, o, bj);
+    } else {
+      o.x = c.one;
+      o.y = c.one;
+      o.z = 0u;
+    }
+    return;
+  }
+  const uint32_t zh = add(a.z, H);
+  uint32_t HH, R2, ZH2;
+  mul4(c, HH, R2, ZH2, d, H, H, rr, rr, zh, zh, zh, zh);
+  const uint32_t I = small(HH, 4);
+  uint32_t Jv, V;
+  mul4(c, Jv, V, d, d1, H, I, a.x, I, H, I, H, I);
+  const uint32_t X3 = sub<2>(c, R2, add(Jv, small(V, 2)));  // < 5.0004
+  const uint32_t w = sub<3>(c, V, X3);
+  uint32_t rw, yj;
+  mul4(c, rw, yj, d, d1, rr, w, a.y, Jv, rr, w, rr, w);
+  o.x = X3;
+  o.y = sub<2>(c, rw, small(yj, 2));
+  o.z = sub<2>(c, ZH2, add(zz, HH));
+}
+
 // x^(p-2) = (x^((p-3)/4))^4 x: the inverse of a nonzero x (every row, redundantly)
 __device__ __forceinline__ uint32_t inv(const Ctx &c, uint32_t x) {
   uint32_t a = dfp::pow_pm3d4(x, c.t);

@@ -697,14 +697,15 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     launch_mv_g2mul(side2, sigs, rands, N, c.R.as<g2j>());
   }
   if (!msm) {
-    HIPCHK(hipStreamWaitEvent(side2, c.ev_pks, 0));
     StageTimer t(S_G2SUM, side2);
-    if (single)
+    if (single) {
+      HIPCHK(hipStreamWaitEvent(side2, c.ev_pks, 0));
       launch_single_S(side2, sigs, pks, pre, pre2, N, c.P.as<g1s>(), c.H.as<g2a>(), seg_err);
-    else
+    } else {  // the signature sums start at once; only their key flags wait for side 1
       launch_g2sum(side2, c.R.as<g2j>(), T + chunk_off, (uint32_t)nchunks, T + segchunk_off,
                    T + segoff_at, NS, N, pks, rands, pre, pre2, empty_is_error, gpart, gpart_err,
-                   c.P.as<g1s>(), c.H.as<g2a>(), seg_err, sj);
+                   c.P.as<g1s>(), c.H.as<g2a>(), seg_err, sj, c.ev_pks);
+    }
   }
   {  // the extra pairs' lines of the first event slice (all events when not sliced)
     StageTimer t(S_LINES_S, side2);

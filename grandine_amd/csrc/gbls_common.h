@@ -79,7 +79,7 @@ void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                   const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
                   int empty_is_error, g2j *part, int32_t *part_err, g1s *P, g2a *H,
-                  int32_t *seg_err, g2j *Sj = nullptr);
+                  int32_t *seg_err, g2j *Sj = nullptr, hipEvent_t keys_ready = nullptr);
 // single checks (r = 1, one set per segment): the extra pair of segment s is (-g1, sig_s)
 void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
                      const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err);

@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32
     g2j r = R[(size_t)h * n + i];
     gang_add(acc, acc, r, q);
     if (h == 0 && q == 0)
-      bad |= (aff_is_inf(pks[i]) || (rands && rands[i] == 0) || (pre && pre[i] != 0) ||
+      bad |= ((pks && aff_is_inf(pks[i])) || (rands && rands[i] == 0) || (pre && pre[i] != 0) ||
               (pre2 && pre2[i] != 0))
                  ? 1
                  : 0;
@@ -121,6 +121,24 @@ __global__ void __launch_bounds__(WGR) k_g2sum_chunks(const g2j *R, const uint32
     part[c] = acc;
     part_err[c] = e_sh;
   }
+}
+
+// the key-side flags of level 1's chunks (an infinite key, a failed key pre-check), ORed into
+// part_err: lets level 1 start before the keys are resolved on the other side stream
+__global__ void __launch_bounds__(WGR) k_g2sum_flags(const uint32_t *chunks, const g1a *pks,
+                                                     const int32_t *pre, int32_t *part_err) {
+  __shared__ int32_t e_sh;
+  const uint32_t c = blockIdx.x;
+  const uint32_t h = chunks[4 * c + 1], b = chunks[4 * c + 2], e = chunks[4 * c + 3];
+  if (threadIdx.x == 0) e_sh = 0;
+  __syncthreads();
+  int32_t bad = 0;
+  if (h == 0)
+    for (uint32_t i = b + threadIdx.x; i < e; i += WGR)
+      bad |= (aff_is_inf(pks[i]) || (pre && pre[i] != 0)) ? 1 : 0;
+  if (bad) atomicOr(&e_sh, 1);
+  __syncthreads();
+  if (threadIdx.x == 0 && e_sh) part_err[c] |= 1;
 }
 
 // level 2: one lane per segment: S = S_lo + [2^32] S_hi over the segment's chunks, then
@@ -221,8 +239,54 @@ __global__ void __launch_bounds__(WG) k_mv_g1mul_lane(const g1a *pks, const uint
   P[i] = o;
 }
 
+// P_i = r_i pk_i, one wave per set (bls_w4.h dbl1 / madd1: three rounds per doubling, six
+// per addition), written as the line-evaluation point (X Z, Y, Z^3) -- the latency regime
+template <bool X>
+__global__ void __launch_bounds__(64) k_mv_g1mul_w4(const g1a *pks, const uint64_t *rands, uint32_t n,
+                                                    g1s *P) {
+  if constexpr (X) w4::exclusive_simd();
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;  // whole waves
+  const g1a pk = pks[i];
+  const uint64_t k = rands[i];
+  const uint32_t j = threadIdx.x & 15, r = (threadIdx.x >> 4) & 3;
+  if (k == 0 || aff_is_inf(pk)) {  // g1s_from_jac of infinity: all zero
+    if (j < 12 && r == 0) {
+      P[i].x.l[j] = 0;
+      P[i].y.l[j] = 0;
+      P[i].c.l[j] = 0;
+    }
+    return;
+  }
+  w4::Ctx c;
+  w4::init(c);
+  const uint32_t cin = dfp::konst(dfp::K_CIN);
+  uint32_t x2, y2, d0, d1;
+  w4::mul4(c, x2, y2, d0, d1, w4::repack(pk.x, j), cin, w4::repack(pk.y, j), cin, w4::repack(pk.x, j), cin,
+           w4::repack(pk.y, j), cin);
+  w4::J1 acc{x2, y2, c.one};
+  const int top = 63 - __clzll((long long)k);
+  for (int bit = top - 1; bit >= 0; bit--) {
+    w4::dbl1(c, acc, acc);
+    if ((k >> bit) & 1) w4::madd1(c, acc, acc, x2, y2);
+  }
+  // (X Z, Y, Z^3): Z = 0 (infinity) gives all-zero x and c, as g1s_from_jac
+  uint32_t xz, z2;
+  w4::mul4(c, xz, z2, d0, d1, acc.x, acc.z, acc.z, acc.z, acc.x, acc.z, acc.x, acc.z);
+  uint32_t z3;
+  w4::mul4(c, z3, d0, d1, d1, z2, acc.z, z2, acc.z, z2, acc.z, z2, acc.z);
+  const uint32_t w = dfp::word_of(w4::sel(c, xz, acc.y, z3, z3), c.t);
+  if (j < 12 && r == 0) P[i].x.l[j] = w;
+  if (j < 12 && r == 1) P[i].y.l[j] = w;
+  if (j < 12 && r == 2) P[i].c.l[j] = w;
+}
+
 void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1s *P) {
   if (!n) return;
+  if (rands && n <= kW4Max) {
+    (n <= w4::kExclusiveMaxWaves ? k_mv_g1mul_w4<true> : k_mv_g1mul_w4<false>)<<<n, 64, 0, st>>>(pks, rands, n, P);
+    return;
+  }
   if (n >= kLaneRegimeSets)
     k_mv_g1mul_lane<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
   else
@@ -328,9 +392,15 @@ void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t
                   const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                   const g1a *pks, const uint64_t *rands, const int32_t *pre, const int32_t *pre2,
                   int empty_is_error, g2j *part, int32_t *part_err, g1s *P, g2a *H,
-                  int32_t *seg_err, g2j *Sj) {
-  if (nchunks)
+                  int32_t *seg_err, g2j *Sj, hipEvent_t keys_ready) {
+  if (keys_ready) {  // level 1 before the keys, their flags after
+    if (nchunks) k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, nullptr, rands, nullptr, pre2, part, part_err);
+    (void)hipStreamWaitEvent(st, keys_ready, 0);
+    if (nchunks) k_g2sum_flags<<<nchunks, WGR, 0, st>>>(chunks, pks, pre, part_err);
+  } else if (nchunks) {
     k_g2sum_chunks<<<nchunks, WGR, 0, st>>>(R, chunks, n, pks, rands, pre, pre2, part, part_err);
+  }
+
   if (nseg && nseg <= kW4Max)
     (nseg <= w4::kExclusiveMaxWaves ? k_g2sum_final_w4<true> : k_g2sum_final_w4<false>)<<<nseg, 64, 0, st>>>(
         part, part_err, chunks, seg_chunk, seg_off, nseg, n,

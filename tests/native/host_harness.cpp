@@ -9,6 +9,7 @@
 #include "../../grandine_amd/csrc/bls_pairing.h"
 #include "../../grandine_amd/csrc/bls_wave12.h"
 #include "../../grandine_amd/csrc/bls_field28.h"
+#include "../../grandine_amd/csrc/bls_curve28.h"
 
 using namespace gbls;
 
@@ -451,6 +452,23 @@ int h_multi_verify(const uint8_t *msgs32, const uint8_t *sigs192, const uint8_t 
   int32_t v;
   pipeline(msgs32, nullptr, sigs192, pks96, rands, nullptr, n, soff, 1, &v);
   return v;
+}
+
+// the lane-regime cofactor clearing in the radix-2^28 layer (bls_curve28.h) against the
+// engine's (bls_hash.h clear_cofactor_g2) on Q0 + Q1 of a message: 1 when the points agree
+int h_r28_clear_check(const uint8_t *msg, uint32_t len) {
+  fp2 u[2];
+  hash_to_field_g2(u, msg, len, dst_ref{POP, 43});
+  g2j q0, q1, want, got;
+  map_to_g2(q0, u[0]);
+  map_to_g2(q1, u[1]);
+  jac_add(q0, q0, q1);
+  clear_cofactor_g2(want, q0);
+  r28::g2j28 a, h;
+  r28::g2j_in(a, q0);
+  r28::clear_cofactor28(h, a);
+  r28::g2j_out(got, h);
+  return jac_eq(got, want) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -233,3 +233,13 @@ def test_radix28_sparse_miller_products(H):
     differs from line_eval_s by one scalar shared by all coefficients."""
     H.h_r28_tower_check.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
     assert H.h_r28_tower_check(7, 30, 40) == 0
+
+
+def test_radix28_cofactor_clearing(H):
+    """The lane-regime cofactor clearing in the radix-2^28 layer (bls_curve28.h: the engine's
+    Jacobian templates over r28::fe2, psi / psi^2 with radix-2^28 constants) equals the
+    engine's clear_cofactor_g2 on Q0 + Q1 of seeded messages."""
+    H.h_r28_clear_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+    for i in range(4):
+        m = b"r28-clear/%d" % i
+        assert H.h_r28_clear_check(m, len(m)) == 1, i
