@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <chrono>
 #include <mutex>
 #include <shared_mutex>
 #include <vector>
@@ -961,6 +962,9 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
 // merged gossip submissions stay below one C2 step (~17 ms of GPU time), so a block-import
 // submission never waits long behind one
 constexpr size_t kMaxMergedSets = 1 << 16;
+// collection window of a new leader while another submission is in flight (see below)
+constexpr size_t kMergeTargetSets = 512;
+constexpr int kMergeWindowUs = 300;
 // Block import (GBLS_CALL_BLOCK, transition_functions/src/deneb/state_transition.rs:69-71
 // verifies a block's signatures on the critical path of its import) has its own queue and
 // leader slot per device: it never waits for a normal leader, is merged only with other
@@ -1074,8 +1078,25 @@ bool coalesced_verify(CoReq &r) {
   int &leaders = r.prio ? co.pleaders : co.leaders;
   std::unique_lock<std::mutex> lk(co.mu);
   q.push_back(&r);
+  co.cv.notify_all();  // a leader collecting a batch (below) sees the new request at once
+  bool waited = false;
   while (!r.done) {
     if (leaders < max_leaders && !q.empty()) {
+      // Another submission is already in flight: the GPU is busy, so a short collection
+      // window costs little latency and lets the callers that return from that submission
+      // join this one (without it the first of them leads a batch of one).  Never for block
+      // import, never on an idle engine.
+      auto queued = [&q]() {
+        size_t t = 0;
+        for (const CoReq *x : q) t += x->n;
+        return t;
+      };
+      if (!r.prio && leaders > 0 && !waited && queued() < kMergeTargetSets) {
+        waited = true;
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(kMergeWindowUs);
+        co.cv.wait_until(lk, deadline, [&] { return r.done || queued() >= kMergeTargetSets; });
+        continue;
+      }
       leaders++;
       std::vector<CoReq *> batch;
       auto mine = std::find(q.begin(), q.end(), &r);

@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(64) k_g2sum_final_w4(const g2j *part, const in
 
 void launch_mv_g2mul(hipStream_t st, const g2a *sigs, const uint64_t *rands, uint32_t n, g2j *R) {
   if (!n) return;
-  if (2 * n <= kW4Max)
+  if (n <= kW4Max)  // 2n waves: up to two per SIMD, still ahead of the quads' one-lane chains
     (2 * n <= w4::kExclusiveMaxWaves ? k_mv_g2mul_w4<true> : k_mv_g2mul_w4<false>)<<<2 * n, 64, 0, st>>>(
         sigs, rands, n, R);
   else
