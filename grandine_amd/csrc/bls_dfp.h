@@ -263,6 +263,58 @@ __device__ __forceinline__ uint32_t word_of(uint32_t x, const Tabs &t) {
   }
   return word;
 }
+// word j of the canonical residue of the row value v = x 2^448 mod p itself, WITHOUT the
+// 2^-64 conversion product: read as engine form it is the element x 2^64 (an Fp* scale
+// factor -- for Miller line coefficients, which the final exponentiation cleans).  v < 2^392
+// (any lazy sum): one estimated multiple of p off (q = top limb / (p_13 + 1)), then at most
+// two conditional subtractions.
+__device__ __forceinline__ uint32_t word_of_scaled(uint32_t x) {
+  uint32_t l[16];
+  For<0, 16>::run([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    l[i] = bcast<i>(x);
+  });
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t v = l[i] + c;
+    c = v >> 28;
+    l[i] = v & M28;
+  }
+  // v < 2^392: limbs 14, 15 are zero; v - q p >= 0 and < p + 2^364 (q <= v / ((p_13 + 1) 2^364))
+  const uint32_t q = l[13] / (K_P_U[13] + 1u);
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const int64_t v = (int64_t)l[i] - (int64_t)q * K_P_U[i] + br;
+    l[i] = (uint32_t)v & M28;
+    br = v >> 28;  // arithmetic shift: the borrow
+  }
+#pragma unroll
+  for (int rep = 0; rep < 2; rep++) {
+    uint32_t d[14];
+    int32_t b2 = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int32_t v = (int32_t)l[i] - (int32_t)K_P_U[i] + b2;
+      b2 = v >> 28;
+      d[i] = (uint32_t)v & M28;
+    }
+    const bool ge = b2 == 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) l[i] = ge ? d[i] : l[i];
+  }
+  const uint32_t j = threadIdx.x & 15;
+  uint32_t word = 0;
+  if (j < 12) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int lo_bit = 28 * i - 32 * (int)j;
+      if (lo_bit > -28 && lo_bit < 32) word |= lo_bit >= 0 ? (l[i] << lo_bit) : (l[i] >> -lo_bit);
+    }
+  }
+  return word;
+}
 __device__ __forceinline__ void to_words(uint32_t *w, uint32_t x, const Tabs &t) {
   const uint32_t word = word_of(x, t);
   if (t.j < 12) w[t.j] = word;

@@ -121,10 +121,12 @@ __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first,
 // row-distributed products, the six line words two more (canonical engine form, SoA as above)
 __device__ __forceinline__ void line_put_w4(const w4::Ctx &c, uint32_t *L, uint32_t np, uint32_t pair,
                                             int e, const w4::f2 &l0, const w4::f2 &l2, const w4::f2 &l3) {
+  // the coefficients times 2^64 (dfp::word_of_scaled: no conversion product; an Fp* factor per
+  // line, which the final exponentiation removes)
   const uint32_t j = c.t.j;
-  uint32_t w = dfp::word_of(w4::sel(c, l0.c0, l0.c1, l2.c0, l2.c1), c.t);
+  uint32_t w = dfp::word_of_scaled(w4::sel(c, l0.c0, l0.c1, l2.c0, l2.c1));
   if (j < 12) L[line_word(e, (int)c.r, (int)j, np, pair)] = w;
-  w = dfp::word_of(w4::sel(c, l3.c0, l3.c1, l3.c0, l3.c1), c.t);
+  w = dfp::word_of_scaled(w4::sel(c, l3.c0, l3.c1, l3.c0, l3.c1));
   if (j < 12 && c.r < 2) L[line_word(e, 4 + (int)c.r, (int)j, np, pair)] = w;
 }
 template <bool X>
