@@ -344,13 +344,30 @@ def main():
         def verdict_ok():
             return bool(torch.equal(d_v.cpu(), want))
 
-        leg.stage_units = lambda s: {"k_g1_aggregate_idx": m * k, "k_lines_S": m, "k_ml_group": 2 * m,
-                                     "k_ml_reduce": 2 * m}.get(s, m)
-        # per message: key aggregation, sigma subgroup check, hash_to_G2, 2 pairs, Horner,
-        # final exponentiation
-        leg.path_fpmul = lambda: m * ((k - 1) * W_FPMUL["k_g1_aggregate_idx"] + W_G2_CHECK
-                                      + W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"] + 2 * W_PAIR
-                                      + W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"])
+        # Batches of 2048..65536 checks take the grouped form (gbls_capi.hip grouped_verdicts):
+        # r_i-weighted pairs, one Horner step + final exponentiation per group of GROUP checks,
+        # then every member of a failing group re-checked on its own (its 2 pairs' Miller
+        # products, Horner step and final exponentiation again).  The work counted is that.
+        GROUP = 8
+        if 2048 <= m <= 65536:
+            bad_groups = {i // GROUP for i in invalid}
+            redo = sum(min(GROUP, m - GROUP * g) for g in bad_groups)
+            segs, g1muls = (m + GROUP - 1) // GROUP + redo, 2 * m
+        else:
+            redo, segs, g1muls = 0, m, 0
+        leg.stage_units = lambda s: {"k_g1_aggregate_idx": m * k, "k_lines_S": m,
+                                     "k_ml_group": 2 * m + 2 * redo, "k_ml_reduce": 2 * m + 2 * redo,
+                                     "k_ml_horner": segs, "k_final_verdict": segs,
+                                     "k_mv_g1mul": max(g1muls // 2, 1)}.get(s, m)
+        # per message: key aggregation, sigma subgroup check, hash_to_G2, 2 pairs (+ the G1
+        # weights); per Miller segment: Horner step, final exponentiation; per re-check: the
+        # 2 pairs' Miller products again
+        leg.path_fpmul = lambda: (m * ((k - 1) * W_FPMUL["k_g1_aggregate_idx"] + W_G2_CHECK
+                                       + W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"] + 2 * W_PAIR)
+                                  + g1muls * W_FPMUL["k_mv_g1mul"]
+                                  + segs * (W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"])
+                                  + redo * 2 * (W_PAIR - W_FPMUL["k_lines"]))
+        leg.grouped = {"checks_per_group": GROUP, "miller_segments": segs, "rechecked": redo} if g1muls else None
     # ------------------------------------------------------------------ C1 (latency, host ABI)
     else:
         return bench_c1(args, L, G, F, np)
@@ -470,6 +487,8 @@ def main():
             line["pairings_per_s"] = round(world * (leg.units + leg.segments) * args.steps / dt, 1)
         if single:
             line["single_batch"] = single
+        if getattr(leg, "grouped", None):
+            line["config"]["grouped_checks"] = leg.grouped
         if cfg == "C4":
             line["pks_aggregated_per_s"] = round(world * leg.pks_per_step * args.steps / dt, 1)
         print(json.dumps(line), flush=True)

@@ -81,8 +81,14 @@ void launch_g2sum(hipStream_t st, const g2j *R, const uint32_t *chunks, uint32_t
                   int empty_is_error, g2j *part, int32_t *part_err, g1s *P, g2a *H,
                   int32_t *seg_err, g2j *Sj = nullptr, hipEvent_t keys_ready = nullptr);
 // single checks (r = 1, one set per segment): the extra pair of segment s is (-g1, sig_s)
+// ng1_out: grouped single checks -- -g1 (affine) per check into ng1_out instead of the
+// pair's G1 point P[n + i], which the caller then scales by r_i (launch_mv_g1mul)
 void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
-                     const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err);
+                     const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err,
+                     g1a *ng1_out = nullptr);
+// gerr[g] = OR of err[i] over the checks [g gs, (g + 1) gs) of group g
+void launch_group_err(hipStream_t st, const int32_t *err, uint32_t n, uint32_t gs, uint32_t ngrp,
+                      int32_t *gerr);
 
 // k_msm.hip -- S_s = sum r_i sig_i of every segment by a signed-digit bucket MSM
 struct MsmPlan {

@@ -204,21 +204,43 @@ __global__ void __launch_bounds__(WG) k_g2sum_final(const g2j *part, const int32
 // S_s = sig_s, so the segment's extra pair is (-g1, sig_s) -- no G2 sum, no inversion.
 __global__ void __launch_bounds__(WG) k_single_S(const g2a *sigs, const g1a *pks, const int32_t *pre,
                                                  const int32_t *pre2, uint32_t n, g1s *P, g2a *H,
-                                                 int32_t *seg_err) {
+                                                 int32_t *seg_err, g1a *ng1_out) {
   uint32_t s = blockIdx.x * WG + threadIdx.x;
   if (s >= n) return;
-  g1s ng1;
-  fp_set(ng1.x, k::G1X_M);
-  fp_set(ng1.y, k::G1NEGY_M);
-  fp_one(ng1.c);
-  P[n + s] = ng1;
+  if (ng1_out) {  // grouped checks: -g1 as the base of the scaled pair (k_mv_g1mul writes P)
+    g1a a;
+    fp_set(a.x, k::G1X_M);
+    fp_set(a.y, k::G1NEGY_M);
+    ng1_out[s] = a;
+  } else {
+    g1s ng1;
+    fp_set(ng1.x, k::G1X_M);
+    fp_set(ng1.y, k::G1NEGY_M);
+    fp_one(ng1.c);
+    P[n + s] = ng1;
+  }
   H[n + s] = sigs[s];
   seg_err[s] = (aff_is_inf(pks[s]) || (pre && pre[s] != 0) || (pre2 && pre2[s] != 0)) ? 1 : 0;
 }
 
 void launch_single_S(hipStream_t st, const g2a *sigs, const g1a *pks, const int32_t *pre,
-                     const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err) {
-  if (n) k_single_S<<<nblk(n), WG, 0, st>>>(sigs, pks, pre, pre2, n, P, H, seg_err);
+                     const int32_t *pre2, uint32_t n, g1s *P, g2a *H, int32_t *seg_err,
+                     g1a *ng1_out) {
+  if (n) k_single_S<<<nblk(n), WG, 0, st>>>(sigs, pks, pre, pre2, n, P, H, seg_err, ng1_out);
+}
+
+// grouped single checks: the error flag of each group of gs checks (any member's)
+__global__ void __launch_bounds__(WG) k_group_err(const int32_t *err, uint32_t n, uint32_t gs,
+                                                  uint32_t ngrp, int32_t *gerr) {
+  const uint32_t gi = blockIdx.x * WG + threadIdx.x;
+  if (gi >= ngrp) return;
+  int32_t bad = 0;
+  for (uint32_t i = gi * gs; i < min(n, (gi + 1) * gs); i++) bad |= err[i];
+  gerr[gi] = bad;
+}
+void launch_group_err(hipStream_t st, const int32_t *err, uint32_t n, uint32_t gs, uint32_t ngrp,
+                      int32_t *gerr) {
+  if (ngrp) k_group_err<<<nblk(ngrp), WG, 0, st>>>(err, n, gs, ngrp, gerr);
 }
 
 // Throughput variant for large batches (every SIMD already busy): one lane per set,

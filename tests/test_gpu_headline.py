@@ -196,3 +196,63 @@ def test_fast_aggregate_verify_golden_batch(G, L):
                                                G.buf(b"".join(keys)), G.u32_array(koff), m, v), "fav_batch")
     for i, c in enumerate(cases):
         assert (v[i] == G.SUCCESS) == c["expect"], c["note"]
+
+
+def test_fast_aggregate_verify_grouped_matches_single_checks(G, L, F):
+    """Batches of >= 2048 independent checks take the grouped form (gbls_capi.hip
+    grouped_verdicts: random G1-side weights, eight checks per final exponentiation, every
+    member of a failing or flagged group re-checked on its own).  On one 4096-check batch with
+    dense and clustered failures -- 20 % flipped messages, one group of eight all invalid, and
+    every golden fast_aggregate_verify case (infinite signature, signature not in G2, missing /
+    no / cancelling / infinity member keys) placed at group boundaries and inside groups --
+    each verdict equals the per-check form's (the same bytes in calls of < 2048 checks) and
+    the construction's expectation."""
+    from grandine_amd import bls as B
+    n = 4096
+    msgs, sigs, pks, _ = F.c2_batch(n, seed=3030)
+    rng = random.Random(3030)
+    sig_l = [sigs[192 * i:192 * (i + 1)] for i in range(n)]
+    msg_l = [msgs[32 * i:32 * (i + 1)] for i in range(n)]
+    key_l = [[pks[96 * i:96 * (i + 1)]] for i in range(n)]
+    expect = [True] * n
+    for i in list(range(40, 48)) + rng.sample(range(64, n), n // 5):  # flipped messages
+        m = bytearray(msg_l[i])
+        m[3] ^= 0x40
+        msg_l[i] = bytes(m)
+        expect[i] = False
+    with open(os.path.join(ROOT, "tests", "golden", "fast_aggregate_verify.json")) as fh:
+        cases = json.load(fh)["cases"]
+    slots = [8 * g + (g % 8) for g in range(100, 100 + 6 * len(cases))]  # every position in a group
+    for j, i in enumerate(slots):
+        c = cases[j % len(cases)]
+        sig_l[i] = B.Signature.try_from(bytes.fromhex(c["sig"])).raw
+        msg_l[i] = bytes.fromhex(c["msg"])
+        keys = []
+        for h in c["pks"]:
+            if h == "c0" + "00" * 47:
+                keys.append(bytes(96))
+            else:
+                st, raw = B.decompress_public_keys([bytes.fromhex(h)], validate=False)[0]
+                assert st == 0
+                keys.append(raw)
+        key_l[i] = keys
+        expect[i] = c["expect"]
+
+    def run(b, e):
+        moff, koff, keys = [0], [0], []
+        for i in range(b, e):
+            moff.append(moff[-1] + len(msg_l[i]))
+            keys += key_l[i]
+            koff.append(len(keys))
+        v = G.i32_array(e - b)
+        G.check(L.gbls_fast_aggregate_verify_batch(G.buf(b"".join(sig_l[b:e])), G.buf(b"".join(msg_l[b:e])),
+                                                   G.u32_array(moff), G.buf(b"".join(keys) or bytes(96)),
+                                                   G.u32_array(koff), e - b, v), "fav_batch")
+        return [v[k] for k in range(e - b)]
+
+    grouped = run(0, n)
+    single = []
+    for b in range(0, n, 1024):
+        single += run(b, b + 1024)
+    assert grouped == single
+    assert [x == G.SUCCESS for x in grouped] == expect
