@@ -1,297 +1,350 @@
-//! Raw bindings of `include/grandine_bls_gpu.h`, the C ABI of the MI355X BLS12-381 engine.
+//! Safe API of the MI355X BLS12-381 engine (`include/grandine_bls_gpu.h`).
 //!
-//! Every prototype of the header is declared here with the same name, argument order and
-//! meaning (`tests/test_rust_binding.py` parses both files and checks them against each other).
-//! Point types are byte-compatible with `blst_p1_affine` / `blst_p2_affine` (little-endian
-//! limbs, Montgomery form, all-zero = infinity), so `blst::min_pk::{PublicKey, Signature}`
-//! values cross the boundary by `transmute_copy`; status codes mirror `BLST_ERROR`.
-//! Any device or driver failure is fail-closed (`GBLS_VERIFY_FAIL`, `gbls_last_error()` set).
-#![no_std]
-#![allow(non_camel_case_types)]
+//! Grandine's workspace forbids unsafe code (`unsafe_code = 'forbid'`, reference
+//! `Cargo.toml:65-66`, inherited by `bls/Cargo.toml:6-7`), so EVERY `unsafe` block of the
+//! drop-in lives in this crate, which does not inherit the workspace lints.  The `bls` crate
+//! calls only the safe functions below (`rust/bls_patch/`).
+//!
+//! * `ffi`: the raw prototypes, one per header entry point.
+//! * Slice-taking wrappers that check lengths before the call, so no wrapper can hand the
+//!   engine a pointer/length pair that does not describe a live Rust slice.
+//! * Engine errors are values: every wrapper returns `Err(EngineError)` when the library
+//!   reports a device, driver or argument failure (`gbls_last_error() != GBLS_ERR_NONE`), and
+//!   `Ok(verdict)` only for a real verdict.  The `bls` crate answers `Err` by running the
+//!   original blst body, so a node whose GPU is missing or broken still verifies on the CPU.
+//! * Conversions between blst's raw points (`blst::min_pk::{PublicKey, Signature}`) and the
+//!   engine's point layout go through blst's own uncompressed serialisation, then copy the
+//!   public limb arrays of `blst_fp` / `blst_fp2` field by field: no `transmute`, no reliance
+//!   on the private layout of blst's wrapper types.
+#![deny(unsafe_op_in_unsafe_fn)]
 
-use core::ffi::{c_char, c_int, c_void};
+pub mod ffi;
 
-#[repr(C)]
-#[derive(Clone, Copy, Debug, Default, PartialEq, Eq)]
-pub struct gbls_p1_affine {
-    pub x: [u64; 6],
-    pub y: [u64; 6],
-}
+use core::{ffi::c_int, ptr};
+use std::sync::OnceLock;
 
-#[repr(C)]
-#[derive(Clone, Copy, Debug, Default, PartialEq, Eq)]
-pub struct gbls_p2_affine {
-    pub x: [[u64; 6]; 2],
-    pub y: [[u64; 6]; 2],
-}
+use blst::{
+    blst_fp, blst_fp2, blst_p1_affine, blst_p2_affine,
+    min_pk::{PublicKey as RawPublicKey, Signature as RawSignature},
+    BLST_ERROR,
+};
 
-#[repr(C)]
+pub use ffi::{gbls_p1_affine as P1, gbls_p2_affine as P2};
+
+// the engine's 64-bit limbs are blst's limb_t on every target Grandine builds for
+const _: () = assert!(core::mem::size_of::<blst::limb_t>() == 8);
+const _: () = assert!(core::mem::size_of::<P1>() == 96 && core::mem::size_of::<P2>() == 192);
+
+/// Why an engine call produced no verdict (the library's `gbls_last_error` codes).
 #[derive(Clone, Copy, Debug, PartialEq, Eq)]
-pub struct gbls_fp12 {
-    pub c: [[u64; 6]; 12],
+pub enum EngineError {
+    /// no usable gfx950 device (or `gbls_init` failed)
+    NoDevice,
+    /// a HIP runtime / driver failure during the call
+    Hip,
+    /// arguments the engine rejects (lengths, offsets, sizes past its limits)
+    Argument,
+    /// any other code (a newer library)
+    Other(i32),
 }
 
-// status codes (BLST_ERROR mirror)
-pub const GBLS_SUCCESS: c_int = 0;
-pub const GBLS_BAD_ENCODING: c_int = 1;
-pub const GBLS_POINT_NOT_ON_CURVE: c_int = 2;
-pub const GBLS_POINT_NOT_IN_GROUP: c_int = 3;
-pub const GBLS_AGGR_TYPE_MISMATCH: c_int = 4;
-pub const GBLS_VERIFY_FAIL: c_int = 5;
-pub const GBLS_PK_IS_INFINITY: c_int = 6;
-pub const GBLS_BAD_SCALAR: c_int = 7;
-// gbls_last_error codes
-pub const GBLS_ERR_NONE: c_int = 0;
-pub const GBLS_ERR_NO_DEVICE: c_int = 100;
-pub const GBLS_ERR_HIP: c_int = 101;
-pub const GBLS_ERR_ARG: c_int = 102;
-// gbls_init flags
-pub const GBLS_INIT_NO_COALESCE: u32 = 0x100;
-pub const GBLS_INIT_TUNING: u32 = 0x200;
-// gbls_multi_verify_compressed_ex call flags
-pub const GBLS_CALL_BLOCK: u32 = 0x1;
+impl EngineError {
+    fn from_code(code: c_int) -> Self {
+        match code {
+            ffi::GBLS_ERR_NO_DEVICE => Self::NoDevice,
+            ffi::GBLS_ERR_HIP => Self::Hip,
+            ffi::GBLS_ERR_ARG => Self::Argument,
+            other => Self::Other(other),
+        }
+    }
+}
 
-extern "C" {
-    pub fn gbls_init(device_mask: u32, flags: u32) -> c_int;
-    pub fn gbls_last_error() -> c_int;
-    pub fn gbls_version() -> *const c_char;
-    pub fn gbls_device_count() -> c_int;
+pub type EngineResult<T> = Result<T, EngineError>;
 
-    // a9 / a8 / a10
-    pub fn gbls_g1_decompress(
-        inp: *const [u8; 48],
-        n: usize,
-        validate: c_int,
-        out: *mut gbls_p1_affine,
-        status: *mut i32,
-    ) -> c_int;
-    pub fn gbls_g2_decompress(
-        inp: *const [u8; 96],
-        n: usize,
-        out: *mut gbls_p2_affine,
-        status: *mut i32,
-    ) -> c_int;
-    pub fn gbls_g2_validate(inp: *const gbls_p2_affine, n: usize, status: *mut i32) -> c_int;
-    pub fn gbls_g1_compress(inp: *const gbls_p1_affine, n: usize, out: *mut [u8; 48]) -> c_int;
-    pub fn gbls_g2_compress(inp: *const gbls_p2_affine, n: usize, out: *mut [u8; 96]) -> c_int;
+/// Call class of a batch verification (the engine's block-import priority class, f3).
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum CallClass {
+    /// gossip, sync committee, API: merged with other normal calls
+    Normal,
+    /// the signatures of a block being imported (its own queue and high-priority streams)
+    BlockImport,
+}
 
-    // a4 / a5 / a11
-    pub fn gbls_g1_aggregate(pks: *const gbls_p1_affine, n: usize, out: *mut gbls_p1_affine) -> c_int;
-    pub fn gbls_g1_aggregate_segments(
-        pks: *const gbls_p1_affine,
-        seg_offsets: *const u32,
-        nseg: usize,
-        out: *mut gbls_p1_affine,
-        status: *mut i32,
-    ) -> c_int;
-    pub fn gbls_g2_aggregate(sigs: *const gbls_p2_affine, n: usize, out: *mut gbls_p2_affine) -> c_int;
-    pub fn gbls_g2_aggregate_segments(
-        sigs: *const gbls_p2_affine,
-        seg_offsets: *const u32,
-        nseg: usize,
-        out: *mut gbls_p2_affine,
-        status: *mut i32,
-    ) -> c_int;
+/// The engine's error code for the call just made on this thread, if any.
+fn last_error() -> Option<EngineError> {
+    // SAFETY: reads a thread-local integer of the library; no arguments.
+    let code = unsafe { ffi::gbls_last_error() };
+    (code != ffi::GBLS_ERR_NONE).then(|| EngineError::from_code(code))
+}
 
-    // f1: device-resident validator registry
-    pub fn gbls_registry_set(first: usize, pks: *const [u8; 48], n: usize, status: *mut i32) -> c_int;
-    pub fn gbls_registry_size() -> usize;
-    pub fn gbls_g1_aggregate_indexed(
-        idx: *const u32,
-        seg_offsets: *const u32,
-        nseg: usize,
-        out: *mut gbls_p1_affine,
-        status: *mut i32,
-    ) -> c_int;
+/// A verification return code -> verdict, or the engine error behind a fail-closed
+/// `GBLS_VERIFY_FAIL`.
+fn verdict(rc: c_int) -> EngineResult<bool> {
+    if let Some(e) = last_error() {
+        return Err(e);
+    }
+    match rc {
+        ffi::GBLS_SUCCESS => Ok(true),
+        ffi::GBLS_VERIFY_FAIL => Ok(false),
+        other => Err(EngineError::Other(other)),
+    }
+}
 
-    // a6 / a7
-    pub fn gbls_verify(
-        sig: *const gbls_p2_affine,
-        msg: *const u8,
-        msg_len: usize,
-        pk: *const gbls_p1_affine,
-    ) -> c_int;
-    pub fn gbls_fast_aggregate_verify(
-        sig: *const gbls_p2_affine,
-        msg: *const u8,
-        msg_len: usize,
-        pks: *const gbls_p1_affine,
-        n: usize,
-    ) -> c_int;
-    pub fn gbls_aggregate_verify_batch(
-        sigs: *const gbls_p2_affine,
-        msg_data: *const u8,
-        msg_off: *const u32,
-        pks: *const gbls_p1_affine,
-        m: usize,
-        verdicts: *mut i32,
-    ) -> c_int;
-    pub fn gbls_fast_aggregate_verify_batch(
-        sigs: *const gbls_p2_affine,
-        msg_data: *const u8,
-        msg_off: *const u32,
-        pks: *const gbls_p1_affine,
-        seg_off: *const u32,
-        m: usize,
-        verdicts: *mut i32,
-    ) -> c_int;
-    pub fn gbls_fast_aggregate_verify_indexed(
-        sigs: *const gbls_p2_affine,
-        msg_data: *const u8,
-        msg_off: *const u32,
-        pk_idx: *const u32,
-        seg_off: *const u32,
-        m: usize,
-        verdicts: *mut i32,
-    ) -> c_int;
+/// A non-verification return code -> `()` or the engine error.
+fn status(rc: c_int) -> EngineResult<()> {
+    if let Some(e) = last_error() {
+        return Err(e);
+    }
+    if rc == ffi::GBLS_SUCCESS {
+        Ok(())
+    } else {
+        Err(EngineError::Other(rc))
+    }
+}
 
-    // a1 / a2 / f2 / f3
-    pub fn gbls_multi_verify(
-        msgs: *const [u8; 32],
-        sigs: *const gbls_p2_affine,
-        pks: *const gbls_p1_affine,
-        rands: *const u64,
-        n: usize,
-    ) -> c_int;
-    pub fn gbls_multi_verify_segments(
-        msgs: *const [u8; 32],
-        sigs: *const gbls_p2_affine,
-        pks: *const gbls_p1_affine,
-        rands: *const u64,
-        n: usize,
-        seg_off: *const u32,
-        nseg: usize,
-        verdicts: *mut i32,
-    ) -> c_int;
-    pub fn gbls_multi_verify_indexed(
-        msgs: *const [u8; 32],
-        sigs: *const gbls_p2_affine,
-        pk_idx: *const u32,
-        pk_off: *const u32,
-        rands: *const u64,
-        n: usize,
-    ) -> c_int;
-    pub fn gbls_multi_verify_compressed(
-        msgs: *const [u8; 32],
-        sigs: *const [u8; 96],
-        pks: *const gbls_p1_affine,
-        pk_idx: *const u32,
-        pk_off: *const u32,
-        rands: *const u64,
-        n: usize,
-        sig_status: *mut i32,
-    ) -> c_int;
-    pub fn gbls_multi_verify_compressed_ex(
-        msgs: *const [u8; 32],
-        sigs: *const [u8; 96],
-        pks: *const gbls_p1_affine,
-        pk_idx: *const u32,
-        pk_off: *const u32,
-        rands: *const u64,
-        n: usize,
-        sig_status: *mut i32,
-        call_flags: u32,
-    ) -> c_int;
-    pub fn gbls_multi_verify_bisect(
-        msgs: *const [u8; 32],
-        sigs: *const gbls_p2_affine,
-        pks: *const gbls_p1_affine,
-        pk_idx: *const u32,
-        pk_off: *const u32,
-        rands: *const u64,
-        n: usize,
-        set_verdicts: *mut i32,
-    ) -> c_int;
+/// BLST_ERROR of an engine status code (the engine mirrors BLST_ERROR's numbering).
+#[must_use]
+pub fn blst_error(code: i32) -> BLST_ERROR {
+    match code {
+        0 => BLST_ERROR::BLST_SUCCESS,
+        1 => BLST_ERROR::BLST_BAD_ENCODING,
+        2 => BLST_ERROR::BLST_POINT_NOT_ON_CURVE,
+        3 => BLST_ERROR::BLST_POINT_NOT_IN_GROUP,
+        4 => BLST_ERROR::BLST_AGGR_TYPE_MISMATCH,
+        6 => BLST_ERROR::BLST_PK_IS_INFINITY,
+        7 => BLST_ERROR::BLST_BAD_SCALAR,
+        _ => BLST_ERROR::BLST_VERIFY_FAIL,
+    }
+}
 
-    // device-pointer variants (inputs resident in HBM; asynchronous on `stream`)
-    pub fn gbls_multi_verify_segments_device(
-        msgs: *const u8,
-        sigs: *const gbls_p2_affine,
-        pks: *const gbls_p1_affine,
-        rands: *const u64,
-        n: usize,
-        seg_off: *const u32,
-        nseg: usize,
-        verdicts: *mut i32,
-        stream: *mut c_void,
-    ) -> c_int;
-    pub fn gbls_multi_verify_indexed_segments_device(
-        msgs: *const u8,
-        sigs: *const gbls_p2_affine,
-        pk_idx: *const u32,
-        pk_off: *const u32,
-        rands: *const u64,
-        n: usize,
-        seg_off: *const u32,
-        nseg: usize,
-        verdicts: *mut i32,
-        stream: *mut c_void,
-    ) -> c_int;
-    pub fn gbls_fast_aggregate_verify_indexed_device(
-        sigs: *const gbls_p2_affine,
-        msgs: *const u8,
-        pk_idx: *const u32,
-        pk_off: *const u32,
-        m: usize,
-        verdicts: *mut i32,
-        stream: *mut c_void,
-    ) -> c_int;
-    pub fn gbls_multi_verify_partials_device(
-        msgs: *const u8,
-        sigs: *const gbls_p2_affine,
-        pks: *const gbls_p1_affine,
-        rands: *const u64,
-        n: usize,
-        seg_off: *const u32,
-        nseg: usize,
-        partials: *mut gbls_fp12,
-        seg_err: *mut i32,
-        stream: *mut c_void,
-    ) -> c_int;
-    pub fn gbls_multi_verify_indexed_partials_device(
-        msgs: *const u8,
-        sigs: *const gbls_p2_affine,
-        pk_idx: *const u32,
-        pk_off: *const u32,
-        rands: *const u64,
-        n: usize,
-        seg_off: *const u32,
-        nseg: usize,
-        partials: *mut gbls_fp12,
-        seg_err: *mut i32,
-        stream: *mut c_void,
-    ) -> c_int;
-    pub fn gbls_final_verify_partials_device(
-        partials: *const gbls_fp12,
-        seg_err: *const i32,
-        nparts: usize,
-        nseg: usize,
-        verdicts: *mut i32,
-        stream: *mut c_void,
-    ) -> c_int;
+// ------------------------------------------------------------------ engine lifetime
 
-    // a15: fixture generation only (not constant time)
-    pub fn gbls_sk_to_pk(sks: *const [u8; 32], n: usize, out: *mut gbls_p1_affine) -> c_int;
-    pub fn gbls_sign(
-        sks: *const [u8; 32],
-        msg_data: *const u8,
-        msg_off: *const u32,
-        n: usize,
-        out: *mut gbls_p2_affine,
-    ) -> c_int;
-    pub fn gbls_hash_to_g2(
-        msg_data: *const u8,
-        msg_off: *const u32,
-        n: usize,
-        dst: *const u8,
-        dst_len: usize,
-        out: *mut gbls_p2_affine,
-    ) -> c_int;
+static ENGINE: OnceLock<EngineResult<usize>> = OnceLock::new();
 
-    // measurement helpers
-    pub fn gbls_measure_mad64_peak() -> f64;
-    pub fn gbls_profile(enable: c_int) -> c_int;
-    pub fn gbls_profile_read(ms: *mut f64, calls: *mut u32, max_stages: c_int) -> c_int;
-    pub fn gbls_profile_reset();
-    pub fn gbls_stage_name(stage: c_int) -> *const c_char;
+/// Opens the engine once per process on every GPU in `GBLS_DEVICE_MASK` (hex or decimal;
+/// default: every device) and returns the number of engines, or why there is none.  The
+/// result is cached: a node without a usable GPU pays for the probe once and then takes the
+/// CPU path on every call without touching the library again.
+pub fn engine() -> EngineResult<usize> {
+    *ENGINE.get_or_init(|| {
+        let mask = std::env::var("GBLS_DEVICE_MASK")
+            .ok()
+            .and_then(|v| {
+                let v = v.trim();
+                v.strip_prefix("0x")
+                    .map_or_else(|| v.parse().ok(), |h| u32::from_str_radix(h, 16).ok())
+            })
+            .unwrap_or(u32::MAX);
+        // SAFETY: plain integers in; the library serialises its own initialisation.
+        let rc = unsafe { ffi::gbls_init(mask, 0) };
+        status(rc)?;
+        // SAFETY: no arguments.
+        let n = unsafe { ffi::gbls_device_count() };
+        usize::try_from(n).ok().filter(|&n| n > 0).ok_or(EngineError::NoDevice)
+    })
+}
+
+/// `true` when the engine is open (see [`engine`]).
+#[must_use]
+pub fn available() -> bool {
+    engine().is_ok()
+}
+
+// ------------------------------------------------------------------ point conversions
+
+/// Engine layout of a blst public key (uncompressed serialisation -> blst affine point ->
+/// limb copy).  A `PublicKey` always holds a point on the curve, so the decode cannot fail.
+#[must_use]
+pub fn p1_of_public_key(key: &RawPublicKey) -> P1 {
+    let bytes = key.serialize();
+    let mut point = blst_p1_affine::default();
+    // SAFETY: `bytes` is the 96-byte uncompressed encoding blst_p1_deserialize reads;
+    // `point` is a valid output location.
+    let rc = unsafe { blst::blst_p1_deserialize(&mut point, bytes.as_ptr()) };
+    debug_assert_eq!(rc, BLST_ERROR::BLST_SUCCESS);
+    P1 { x: point.x.l, y: point.y.l }
+}
+
+/// blst public key of an engine point (limb copy -> uncompressed serialisation -> blst's own
+/// decoder, which checks that the point is on the curve).
+pub fn public_key_of_p1(point: &P1) -> Result<RawPublicKey, BLST_ERROR> {
+    let affine = blst_p1_affine { x: blst_fp { l: point.x }, y: blst_fp { l: point.y } };
+    let mut bytes = [0_u8; 96];
+    // SAFETY: `bytes` has room for the 96-byte encoding; `affine` is a valid input.
+    unsafe { blst::blst_p1_affine_serialize(bytes.as_mut_ptr(), &affine) };
+    RawPublicKey::deserialize(&bytes)
+}
+
+/// Engine layout of a blst signature (see [`p1_of_public_key`]).
+#[must_use]
+pub fn p2_of_signature(signature: &RawSignature) -> P2 {
+    let bytes = signature.serialize();
+    let mut point = blst_p2_affine::default();
+    // SAFETY: `bytes` is the 192-byte uncompressed encoding blst_p2_deserialize reads.
+    let rc = unsafe { blst::blst_p2_deserialize(&mut point, bytes.as_ptr()) };
+    debug_assert_eq!(rc, BLST_ERROR::BLST_SUCCESS);
+    P2 { x: [point.x.fp[0].l, point.x.fp[1].l], y: [point.y.fp[0].l, point.y.fp[1].l] }
+}
+
+/// blst signature of an engine point (on-curve checked by blst's decoder).
+pub fn signature_of_p2(point: &P2) -> Result<RawSignature, BLST_ERROR> {
+    let fp2 = |c: &[[u64; 6]; 2]| blst_fp2 { fp: [blst_fp { l: c[0] }, blst_fp { l: c[1] }] };
+    let affine = blst_p2_affine { x: fp2(&point.x), y: fp2(&point.y) };
+    let mut bytes = [0_u8; 192];
+    // SAFETY: `bytes` has room for the 192-byte encoding; `affine` is a valid input.
+    unsafe { blst::blst_p2_affine_serialize(bytes.as_mut_ptr(), &affine) };
+    RawSignature::deserialize(&bytes)
+}
+
+// ------------------------------------------------------------------ safe entry points
+
+/// a9: `PublicKey::try_from` (decompression + `validate()` when `validate`).  `Ok(Err(e))` is
+/// the decoder's BLST_ERROR for these bytes; `Err` is an engine failure.
+pub fn g1_decompress(bytes: &[u8; 48], validate: bool) -> EngineResult<Result<P1, BLST_ERROR>> {
+    let mut out = P1::default();
+    let mut st = ffi::GBLS_BAD_ENCODING;
+    // SAFETY: one 48-byte input, one output point and one status, as n = 1 says.
+    let rc = unsafe { ffi::gbls_g1_decompress(bytes, 1, c_int::from(validate), &mut out, &mut st) };
+    status(rc)?;
+    Ok(if st == ffi::GBLS_SUCCESS { Ok(out) } else { Err(blst_error(st)) })
+}
+
+/// a8: `Signature::try_from` (decompression, on-curve, no subgroup check).
+pub fn g2_decompress(bytes: &[u8; 96]) -> EngineResult<Result<P2, BLST_ERROR>> {
+    let mut out = P2::default();
+    let mut st = ffi::GBLS_BAD_ENCODING;
+    // SAFETY: one 96-byte input, one output point and one status, as n = 1 says.
+    let rc = unsafe { ffi::gbls_g2_decompress(bytes, 1, &mut out, &mut st) };
+    status(rc)?;
+    Ok(if st == ffi::GBLS_SUCCESS { Ok(out) } else { Err(blst_error(st)) })
+}
+
+/// a5: the sum of `points` (infinity-aware).  An empty slice is an argument error.
+pub fn g1_aggregate(points: &[P1]) -> EngineResult<P1> {
+    if points.is_empty() {
+        return Err(EngineError::Argument);
+    }
+    let mut out = P1::default();
+    // SAFETY: `points` is a live slice of `points.len()` elements; one output point.
+    let rc = unsafe { ffi::gbls_g1_aggregate(points.as_ptr(), points.len(), &mut out) };
+    status(rc).map(|()| out)
+}
+
+/// a11: the sum of `points` (infinity-aware).  An empty slice is an argument error.
+pub fn g2_aggregate(points: &[P2]) -> EngineResult<P2> {
+    if points.is_empty() {
+        return Err(EngineError::Argument);
+    }
+    let mut out = P2::default();
+    // SAFETY: as in g1_aggregate.
+    let rc = unsafe { ffi::gbls_g2_aggregate(points.as_ptr(), points.len(), &mut out) };
+    status(rc).map(|()| out)
+}
+
+/// a6: `Signature::verify` semantics (signature subgroup check, infinite key rejected).
+pub fn verify(signature: &P2, message: &[u8], key: &P1) -> EngineResult<bool> {
+    // SAFETY: `message` is a live slice of `message.len()` bytes; single points by reference.
+    let rc = unsafe { ffi::gbls_verify(signature, message.as_ptr(), message.len(), key) };
+    verdict(rc)
+}
+
+/// a7: `Signature::fast_aggregate_verify` (no keys -> `Ok(false)`, as blst).
+pub fn fast_aggregate_verify(signature: &P2, message: &[u8], keys: &[P1]) -> EngineResult<bool> {
+    if keys.is_empty() {
+        return Ok(false);
+    }
+    // SAFETY: live slices with their own lengths.
+    let rc = unsafe {
+        ffi::gbls_fast_aggregate_verify(signature, message.as_ptr(), message.len(), keys.as_ptr(), keys.len())
+    };
+    verdict(rc)
+}
+
+/// a1: `Signature::multi_verify` with caller-drawn nonzero scalars.  Slices of different
+/// lengths, an empty batch or a zero scalar are argument errors (the caller falls back).
+pub fn multi_verify(messages: &[[u8; 32]], signatures: &[P2], keys: &[P1], scalars: &[u64]) -> EngineResult<bool> {
+    let n = messages.len();
+    if n == 0 || signatures.len() != n || keys.len() != n || scalars.len() != n || scalars.contains(&0) {
+        return Err(EngineError::Argument);
+    }
+    // SAFETY: four live slices of n elements each.
+    let rc = unsafe {
+        ffi::gbls_multi_verify(messages.as_ptr(), signatures.as_ptr(), keys.as_ptr(), scalars.as_ptr(), n)
+    };
+    verdict(rc)
+}
+
+/// a2: `MultiVerifier::finish` as one submission (96-byte signatures decompressed on the
+/// device).  `Ok(Err(e))`: the first signature that does not decode, with its BLST_ERROR
+/// (finish's `DecompressionFailed`); `Ok(Ok(v))`: the verdict.
+pub fn multi_verify_compressed(
+    messages: &[[u8; 32]],
+    signatures: &[[u8; 96]],
+    keys: &[P1],
+    scalars: &[u64],
+    class: CallClass,
+) -> EngineResult<Result<bool, BLST_ERROR>> {
+    let n = messages.len();
+    if n == 0 || signatures.len() != n || keys.len() != n || scalars.len() != n || scalars.contains(&0) {
+        return Err(EngineError::Argument);
+    }
+    let mut statuses = vec![ffi::GBLS_BAD_ENCODING; n];
+    let flags = match class {
+        CallClass::Normal => 0,
+        CallClass::BlockImport => ffi::GBLS_CALL_BLOCK,
+    };
+    // SAFETY: live slices of n elements each (keys as points: no index arrays).
+    let rc = unsafe {
+        ffi::gbls_multi_verify_compressed_ex(
+            messages.as_ptr(),
+            signatures.as_ptr(),
+            keys.as_ptr(),
+            ptr::null(),
+            ptr::null(),
+            scalars.as_ptr(),
+            n,
+            statuses.as_mut_ptr(),
+            flags,
+        )
+    };
+    if let Some(e) = last_error() {
+        return Err(e);
+    }
+    Ok(match rc {
+        ffi::GBLS_SUCCESS => Ok(true),
+        ffi::GBLS_VERIFY_FAIL => Ok(false),
+        decode => Err(blst_error(decode)),
+    })
+}
+
+/// f2: per-set verdicts of a batch (`true` = the set verifies on its own).
+pub fn multi_verify_bisect(
+    messages: &[[u8; 32]],
+    signatures: &[P2],
+    keys: &[P1],
+    scalars: &[u64],
+) -> EngineResult<Vec<bool>> {
+    let n = messages.len();
+    if signatures.len() != n || keys.len() != n || scalars.len() != n || scalars.contains(&0) {
+        return Err(EngineError::Argument);
+    }
+    if n == 0 {
+        return Ok(Vec::new());
+    }
+    let mut verdicts = vec![ffi::GBLS_VERIFY_FAIL; n];
+    // SAFETY: live slices of n elements each; n verdict slots.
+    let rc = unsafe {
+        ffi::gbls_multi_verify_bisect(
+            messages.as_ptr(),
+            signatures.as_ptr(),
+            keys.as_ptr(),
+            ptr::null(),
+            ptr::null(),
+            scalars.as_ptr(),
+            n,
+            verdicts.as_mut_ptr(),
+        )
+    };
+    status(rc)?;
+    Ok(verdicts.into_iter().map(|v| v == ffi::GBLS_SUCCESS).collect())
 }

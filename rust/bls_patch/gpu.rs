@@ -1,159 +1,81 @@
-//! bls/src/gpu.rs -- the one module of the `bls` crate that talks to the MI355X engine.
+//! bls/src/gpu.rs -- routing between the MI355X engine and blst.
 //!
-//! blst's affine point types have exactly the engine's layout (48-byte little-endian
-//! Montgomery coordinates, all-zero = infinity); the assertions below keep that true at compile
-//! time.  Every wrapper is fail-closed: an engine or device error is a verification failure.
-#![allow(unsafe_code)]
+//! This module contains no unsafe code: the `bls` crate keeps Grandine's workspace lints
+//! (`unsafe_code = 'forbid'`, reference `Cargo.toml:65-66`, `bls/Cargo.toml:6-7`), and every
+//! FFI call and point conversion is a safe function of `bls_gpu_sys`.
+//!
+//! Routing rule: a patched body runs on the engine when it is open and returns a verdict;
+//! when the engine is absent (no gfx950 device, `gbls_init` failed) or a call reports an
+//! engine error (`bls_gpu_sys::EngineError`: HIP/driver failure, argument outside the
+//! engine's limits), the body runs its original blst code instead ("the Rust
+//! shim falls back to the CPU path").  A verdict of the engine is never second-guessed: an
+//! invalid signature is `false` on both paths, and only a missing verdict goes to the CPU.
+//! A failed engine call therefore costs time, never a wrong answer or a silently kept value.
 
-use core::{mem::size_of, ptr};
+use core::sync::atomic::{AtomicU64, Ordering};
 
-use bls_gpu_sys as sys;
-use blst::{blst_p1_affine, blst_p2_affine, BLST_ERROR};
-use static_assertions::assert_eq_size;
+pub use bls_gpu_sys::{CallClass, EngineError, P1, P2};
 
-assert_eq_size!(blst_p1_affine, sys::gbls_p1_affine);
-assert_eq_size!(blst_p2_affine, sys::gbls_p2_affine);
+use crate::{PublicKey, Signature};
 
-/// `gbls_init` once per process (idempotent on the C side): every GPU of the node.
-pub fn init(device_mask: u32) -> bool {
-    unsafe { sys::gbls_init(device_mask, 0) == sys::GBLS_SUCCESS }
+static CPU_FALLBACKS: AtomicU64 = AtomicU64::new(0);
+
+/// Calls that ran on blst because the engine was absent or failed (for metrics / logs).
+#[must_use]
+pub fn cpu_fallbacks() -> u64 {
+    CPU_FALLBACKS.load(Ordering::Relaxed)
 }
 
-#[inline]
-pub(crate) fn p1(p: &blst_p1_affine) -> sys::gbls_p1_affine {
-    unsafe { core::mem::transmute_copy(p) }
+/// `true` when the engine is open (opened on first use; cached for the process).
+#[must_use]
+pub fn available() -> bool {
+    bls_gpu_sys::available()
 }
 
-#[inline]
-pub(crate) fn p2(p: &blst_p2_affine) -> sys::gbls_p2_affine {
-    unsafe { core::mem::transmute_copy(p) }
-}
-
-#[inline]
-pub(crate) fn from_p1(p: &sys::gbls_p1_affine) -> blst_p1_affine {
-    unsafe { core::mem::transmute_copy(p) }
-}
-
-#[inline]
-pub(crate) fn from_p2(p: &sys::gbls_p2_affine) -> blst_p2_affine {
-    unsafe { core::mem::transmute_copy(p) }
-}
-
-/// BLST_ERROR from an engine status code (the engine mirrors BLST_ERROR's numbering).
-/// The engine's view of a public key (for callers outside the crate, e.g. MultiVerifier).
-pub fn public_key_point(pk: &crate::PublicKey) -> sys::gbls_p1_affine {
-    p1(&pk.as_raw().into())
-}
-
-pub(crate) fn blst_error(status: i32) -> BLST_ERROR {
-    match status {
-        0 => BLST_ERROR::BLST_SUCCESS,
-        1 => BLST_ERROR::BLST_BAD_ENCODING,
-        2 => BLST_ERROR::BLST_POINT_NOT_ON_CURVE,
-        3 => BLST_ERROR::BLST_POINT_NOT_IN_GROUP,
-        4 => BLST_ERROR::BLST_AGGR_TYPE_MISMATCH,
-        6 => BLST_ERROR::BLST_PK_IS_INFINITY,
-        7 => BLST_ERROR::BLST_BAD_SCALAR,
-        _ => BLST_ERROR::BLST_VERIFY_FAIL,
+/// Runs `gpu` when the engine is open and takes its result; otherwise, or when it reports an
+/// engine error, runs `cpu` (the original blst body).
+pub(crate) fn route<T>(gpu: impl FnOnce() -> Result<T, EngineError>, cpu: impl FnOnce() -> T) -> T {
+    if available() {
+        if let Ok(value) = gpu() {
+            return value;
+        }
     }
+    CPU_FALLBACKS.fetch_add(1, Ordering::Relaxed);
+    cpu()
 }
 
-pub(crate) fn g1_decompress_validate(bytes: &[u8; 48]) -> Result<blst_p1_affine, BLST_ERROR> {
-    let mut out = sys::gbls_p1_affine::default();
-    let mut status = sys::GBLS_BAD_ENCODING;
-    let rc = unsafe { sys::gbls_g1_decompress(bytes, 1, 1, &mut out, &mut status) };
-    match (rc, status) {
-        (sys::GBLS_SUCCESS, 0) => Ok(from_p1(&out)),
-        (sys::GBLS_SUCCESS, s) => Err(blst_error(s)),
-        _ => Err(BLST_ERROR::BLST_BAD_ENCODING),
-    }
+/// Engine layout of a public key (for callers outside the crate, e.g. `MultiVerifier`).
+#[must_use]
+pub fn public_key_point(public_key: &PublicKey) -> P1 {
+    bls_gpu_sys::p1_of_public_key(public_key.as_raw())
 }
 
-pub(crate) fn g2_decompress(bytes: &[u8; 96]) -> Result<blst_p2_affine, BLST_ERROR> {
-    let mut out = sys::gbls_p2_affine::default();
-    let mut status = sys::GBLS_BAD_ENCODING;
-    let rc = unsafe { sys::gbls_g2_decompress(bytes, 1, &mut out, &mut status) };
-    match (rc, status) {
-        (sys::GBLS_SUCCESS, 0) => Ok(from_p2(&out)),
-        (sys::GBLS_SUCCESS, s) => Err(blst_error(s)),
-        _ => Err(BLST_ERROR::BLST_BAD_ENCODING),
-    }
+/// Engine layout of a signature.
+#[must_use]
+pub fn signature_point(signature: &Signature) -> P2 {
+    bls_gpu_sys::p2_of_signature(signature.as_raw())
 }
 
-pub(crate) fn g1_sum(points: &[sys::gbls_p1_affine]) -> Option<sys::gbls_p1_affine> {
-    let mut out = sys::gbls_p1_affine::default();
-    let rc = unsafe { sys::gbls_g1_aggregate(points.as_ptr(), points.len(), &mut out) };
-    (rc == sys::GBLS_SUCCESS).then_some(out)
-}
-
-pub(crate) fn g2_sum(points: &[sys::gbls_p2_affine]) -> Option<sys::gbls_p2_affine> {
-    let mut out = sys::gbls_p2_affine::default();
-    let rc = unsafe { sys::gbls_g2_aggregate(points.as_ptr(), points.len(), &mut out) };
-    (rc == sys::GBLS_SUCCESS).then_some(out)
-}
-
-pub(crate) fn verify(sig: &blst_p2_affine, msg: &[u8], pk: &blst_p1_affine) -> bool {
-    let (s, p) = (p2(sig), p1(pk));
-    unsafe { sys::gbls_verify(&s, msg.as_ptr(), msg.len(), &p) == sys::GBLS_SUCCESS }
-}
-
-pub(crate) fn fast_aggregate_verify(sig: &blst_p2_affine, msg: &[u8], pks: &[sys::gbls_p1_affine]) -> bool {
-    let s = p2(sig);
-    unsafe {
-        sys::gbls_fast_aggregate_verify(&s, msg.as_ptr(), msg.len(), pks.as_ptr(), pks.len())
-            == sys::GBLS_SUCCESS
-    }
-}
-
-pub(crate) fn multi_verify(
-    msgs: &[[u8; 32]],
-    sigs: &[sys::gbls_p2_affine],
-    pks: &[sys::gbls_p1_affine],
-    rands: &[u64],
-) -> bool {
-    let n = msgs.len();
-    if n == 0 || sigs.len() != n || pks.len() != n || rands.len() != n {
-        return false;
-    }
-    unsafe {
-        sys::gbls_multi_verify(msgs.as_ptr(), sigs.as_ptr(), pks.as_ptr(), rands.as_ptr(), n)
-            == sys::GBLS_SUCCESS
-    }
-}
-
-/// MultiVerifier::finish as one submission: the 96-byte signatures are decompressed on the
-/// device.  Err(first failing status) when a signature does not decode, Ok(verdict) otherwise.
+/// `MultiVerifier::finish` as one engine submission: 96-byte signatures decompressed on the
+/// device, then the random-linear-combination check with the caller's nonzero scalars.
+/// `None`: no engine verdict (absent engine or engine error) -- the caller runs its blst body.
+/// `Some(Err(e))`: a signature does not decode (`DecompressionFailed(e)`);
+/// `Some(Ok(v))`: the verdict.
+#[must_use]
 pub fn multi_verify_compressed(
-    msgs: &[[u8; 32]],
-    sig_bytes: &[[u8; 96]],
-    pks: &[sys::gbls_p1_affine],
-    rands: &[u64],
-    block_import: bool,
-) -> Result<bool, BLST_ERROR> {
-    let n = msgs.len();
-    if n == 0 || sig_bytes.len() != n || pks.len() != n || rands.len() != n {
-        return Ok(false);
+    messages: &[[u8; 32]],
+    signature_bytes: &[[u8; 96]],
+    public_keys: &[P1],
+    scalars: &[u64],
+    class: CallClass,
+) -> Option<Result<bool, blst::BLST_ERROR>> {
+    if !available() {
+        CPU_FALLBACKS.fetch_add(1, Ordering::Relaxed);
+        return None;
     }
-    let mut status = vec![0_i32; n];
-    let flags = if block_import { sys::GBLS_CALL_BLOCK } else { 0 };
-    let rc = unsafe {
-        sys::gbls_multi_verify_compressed_ex(
-            msgs.as_ptr(),
-            sig_bytes.as_ptr(),
-            pks.as_ptr(),
-            ptr::null(),
-            ptr::null(),
-            rands.as_ptr(),
-            n,
-            status.as_mut_ptr(),
-            flags,
-        )
-    };
-    match rc {
-        sys::GBLS_SUCCESS => Ok(true),
-        sys::GBLS_VERIFY_FAIL => Ok(false),
-        s => Err(blst_error(s)),
+    let result = bls_gpu_sys::multi_verify_compressed(messages, signature_bytes, public_keys, scalars, class);
+    if result.is_err() {
+        CPU_FALLBACKS.fetch_add(1, Ordering::Relaxed);
     }
+    result.ok()
 }
-
-const _: () = assert!(size_of::<sys::gbls_p2_affine>() == 192 && size_of::<sys::gbls_p1_affine>() == 96);

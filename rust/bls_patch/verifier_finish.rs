@@ -1,4 +1,5 @@
-// Replacement body of MultiVerifier::finish, helper_functions/src/verifier.rs:301-323.
+// Replacement body of MultiVerifier::finish, helper_functions/src/verifier.rs:301-323.  No
+// unsafe code (helper_functions keeps the workspace's `unsafe_code = 'forbid'`).
 //
 // The reference decompresses every signature on rayon workers (verifier.rs:309-313), then calls
 // Signature::multi_verify.  Here the 96-byte signatures go to the device with the messages, keys
@@ -12,6 +13,7 @@
 //
 // which the block paths pass when they build their verifier
 // (p2p/src/block_verification_pool.rs:109, fork_choice_control/src/tasks.rs:101).
+// Without an engine verdict (no device, engine error) the reference body runs unchanged.
 
 #[inline]
 fn finish(&self) -> Result<()> {
@@ -27,7 +29,7 @@ fn finish(&self) -> Result<()> {
     let signature_bytes = self
         .triples
         .iter()
-        .map(|triple| <[u8; 96]>::try_from(triple.signature_bytes.as_bytes()).expect("96 bytes"))
+        .map(|triple| triple.signature_bytes.to_fixed_bytes())
         .collect_vec();
     let public_keys = self
         .triples
@@ -42,18 +44,38 @@ fn finish(&self) -> Result<()> {
 
     // block verification (transition_functions/src/deneb/state_transition.rs:69-71) is the
     // latency-critical caller; gossip batches go through the normal class
-    let block_import = self.has_option(VerifierOption::BlockImport);
+    let class = if self.has_option(VerifierOption::BlockImport) {
+        bls::gpu::CallClass::BlockImport
+    } else {
+        bls::gpu::CallClass::Normal
+    };
 
-    let verdict = bls::gpu::multi_verify_compressed(
-        &messages,
-        &signature_bytes,
-        &public_keys,
-        &randoms,
-        block_import,
-    )
-    .map_err(bls::Error::DecompressionFailed)?;
+    match bls::gpu::multi_verify_compressed(&messages, &signature_bytes, &public_keys, &randoms, class) {
+        Some(verdict) => {
+            let verdict = verdict.map_err(bls::Error::DecompressionFailed)?;
+            ensure!(verdict, Error::SignatureInvalid(SignatureKind::Multi));
+            Ok(())
+        }
+        None => self.finish_on_cpu(),
+    }
+}
 
-    ensure!(verdict, Error::SignatureInvalid(SignatureKind::Multi));
+// The reference body (verifier.rs:301-323), added to `impl MultiVerifier` as a private method.
+fn finish_on_cpu(&self) -> Result<()> {
+    let messages = self.triples.iter().map(|triple| triple.message.as_bytes());
+
+    let signatures = self
+        .triples
+        .par_iter()
+        .map(|triple| triple.signature_bytes.try_into())
+        .collect::<Result<Vec<_>, _>>()?;
+
+    let public_keys = self.triples.iter().map(|triple| &triple.public_key);
+
+    ensure!(
+        Signature::multi_verify(messages, signatures.iter(), public_keys),
+        Error::SignatureInvalid(SignatureKind::Multi),
+    );
 
     Ok(())
 }
