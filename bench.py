@@ -26,8 +26,9 @@ block (~131 sets) through the host-pointer ABI: latency, plus 64-set gossip batc
 N > 1 (torch.distributed.run, one rank per GPU, backend nccl = RCCL): every rank verifies
 its own sets; the per-rank Miller partial (one Fp12, 576 B) and error flag are
 all-gathered over xGMI, and every rank runs ONE final exponentiation over the product
-(SURVEY.md 8(e)).  C2/C4 are weak scaling (a fixed batch per GPU), C5 strong (2^20 sets
-in total), C3 needs no exchange (per-message verdicts).
+(SURVEY.md 8(e)).  C2 is weak scaling (a fixed batch per GPU); C4 (one mainnet epoch, its
+2048 committees split into whole committees per rank) and C5 (2^20 sets in total) are strong
+scaling; C3 needs no exchange (per-message verdicts).
 
 Extra JSON fields: "roofline" (dominant kernel's integer-multiply throughput vs the
 measured v_mad_u64_u32 peak, HIP events on the launch stream, W frozen in BASELINE.md 4)
@@ -74,6 +75,9 @@ W_SEGMENT = W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"] + W_PAIR        
 W_SET = (W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"] + W_FPMUL["k_mv_g1mul"]
          + W_FPMUL["k_mv_g2mul"] + W_PAIR)                                            # 11815
 W_G2_CHECK = 1251  # sigma subgroup check (fast_aggregate_verify)
+W_C3_MESSAGE = (511 * W_FPMUL["k_g1_aggregate_idx"] + W_G2_CHECK + W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"]
+                + 2 * W_PAIR + W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"])            # 39579
+assert W_C3_MESSAGE == 39579, W_C3_MESSAGE  # BASELINE.md 4, frozen
 
 
 def cpu_threads():
@@ -156,6 +160,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's host CPU share")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-single", action="store_true",
+                    help="C2: skip the one-batch-per-step leg (PMC passes then see only the 16-batch launches)")
     ap.add_argument("--tuning", action="store_true",
                     help="let the engine read its GBLS_* tuning environment variables (sweeps)")
     args = ap.parse_args()
@@ -230,20 +236,30 @@ def main():
                             "C2: %d independent batches of %d single-pubkey sets per GPU per step, each its own "
                             "random-scalar multi_verify (segments of one submission)" % (nb, per))
         elif cfg == "C4":
-            ncom = args.sets or 2048
+            # ONE mainnet epoch (32 slots x 64 committees, reference types/src/preset.rs:158,219),
+            # the same on every rank; rank r verifies whole committees [r C / N, (r+1) C / N) and
+            # the ranks' Miller partials meet in one final exponentiation: strong
+            # scaling, as BASELINE.json configs[3] ("sharded over 8 GPUs")
+            ncom_all = args.sets or 2048
             nreg = 1 << 20
             nact = nreg - 576  # committee sizes 511/512 (a shuffle remainder)
             sks, comp = F.registry(nreg, seed=b"c4-registry")
             assert not F.load_registry(comp).any()
-            idx, off = F.committees(nact, ncom, seed=rank + 4)
-            msgs = F.messages(ncom, b"c4/%d" % rank)
+            idx_all, off_all = F.committees(nact, ncom_all, seed=4)
+            c0, c1 = ncom_all * rank // world, ncom_all * (rank + 1) // world
+            idx = idx_all[off_all[c0]:off_all[c1]]
+            off = (off_all[c0:c1 + 1] - off_all[c0]).astype(np.uint32)
+            msgs = F.messages(ncom_all, b"c4")[32 * c0:32 * c1]
             sigs, _ = F.committee_signatures(sks, idx, off, msgs)
-            rands = F.rands(ncom, rank + 4)
-            n = ncom
+            rands = F.rands(ncom_all, 4)[c0:c1]
+            n = c1 - c0
             leg.pks_per_step = int(off[-1])
-            leg.workload = ("C4: one epoch of attestations per GPU -- %d committees (%d keys, sizes %d-%d) "
-                            "aggregated from a %d-key device registry + one multi_verify"
-                            % (ncom, int(off[-1]), int(np.diff(off).min()), int(np.diff(off).max()), nreg))
+            leg.scaling = "strong"
+            leg.epoch = {"committees": ncom_all, "keys": int(off_all[-1])}
+            leg.workload = ("C4: one mainnet epoch of attestations -- %d committees (%d keys, sizes %d-%d) aggregated "
+                            "from a %d-key device registry + one multi_verify, whole committees split over the GPUs "
+                            "(%d on this rank)" % (ncom_all, int(off_all[-1]), int(np.diff(off_all).min()),
+                                                   int(np.diff(off_all).max()), nreg, n))
         else:
             nreg = 1_700_000
             total = args.sets or (1 << 20)
@@ -359,14 +375,10 @@ def main():
                                      "k_ml_group": 2 * m + 2 * redo, "k_ml_reduce": 2 * m + 2 * redo,
                                      "k_ml_horner": segs, "k_final_verdict": segs,
                                      "k_mv_g1mul": max(g1muls // 2, 1)}.get(s, m)
-        # per message: key aggregation, sigma subgroup check, hash_to_G2, 2 pairs (+ the G1
-        # weights); per Miller segment: Horner step, final exponentiation; per re-check: the
-        # 2 pairs' Miller products again
-        leg.path_fpmul = lambda: (m * ((k - 1) * W_FPMUL["k_g1_aggregate_idx"] + W_G2_CHECK
-                                       + W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"] + 2 * W_PAIR)
-                                  + g1muls * W_FPMUL["k_mv_g1mul"]
-                                  + segs * (W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"])
-                                  + redo * 2 * (W_PAIR - W_FPMUL["k_lines"]))
+        # the whole path at BASELINE.md 4's FROZEN 39,579 Fp products per message (511 key
+        # additions, sigma subgroup check, hash_to_G2, 2 pairs, Horner, final exponentiation):
+        # the grouped form does less work per message, which raises the fraction, never W
+        leg.path_fpmul = lambda: m * W_C3_MESSAGE
         leg.grouped = {"checks_per_group": GROUP, "miller_segments": segs, "rechecked": redo} if g1muls else None
     # ------------------------------------------------------------------ C1 (latency, host ABI)
     else:
@@ -414,9 +426,25 @@ def main():
     if not ok:
         raise SystemExit("verdicts changed during the timed region")
 
+    # ---- C4: every committee's own verdict (each committee one segment), on every rank
+    committee_check = None
+    if cfg == "C4":
+        segc = G.u32_array(range(n + 1))
+        vc = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        G.check(L.gbls_multi_verify_indexed_segments_device(ptr(d_msgs), ptr(d_sigs), ptr(d_idx), ptr(d_off),
+                                                            ptr(d_rands), n, segc, n, ptr(vc), cur_stream()),
+                "per-committee check")
+        torch.cuda.synchronize()
+        good = torch.tensor([int((vc == G.SUCCESS).sum().item())], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(good, op=dist.ReduceOp.SUM)
+        committee_check = {"committees_verified": int(good.item()), "committees": leg.epoch["committees"]}
+        if committee_check["committees_verified"] != leg.epoch["committees"]:
+            raise SystemExit("per-committee verdicts WRONG: %s" % committee_check)
+
     # ---- one batch per step (the 4096-set latency view), same inputs, after the main timing
     single = None
-    if cfg == "C2" and world == 1 and leg.segments > 1:
+    if cfg == "C2" and world == 1 and leg.segments > 1 and not args.no_single:
         per = leg.units // leg.segments
         seg1 = G.u32_array([0, per])
         v1 = torch.full((1,), -1, dtype=torch.int32, device=dev)
@@ -470,7 +498,10 @@ def main():
                 "stage_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()}}
 
     if rank == 0:
-        value = world * leg.units * args.steps / dt if leg.scaling == "weak" else world * leg.units * args.steps / dt
+        # whole-job throughput: every rank's units (C5/C4 strong: the ranks' shares add up to the
+        # one workload; C2 weak: world x the per-GPU batch)
+        total_units = leg.epoch["committees"] if cfg == "C4" else world * leg.units
+        value = total_units * args.steps / dt
         cpu = None
         if not args.no_cpu and world == 1 and cfg == "C2":
             cpu = cpu_baseline(args.cpu_sample, args.cpu_threads or cpu_threads())
@@ -484,13 +515,14 @@ def main():
                            "parallelism": "shard sets, RCCL all-gather of Fp12 partials" if world > 1 else "1 GPU"},
                 "roofline": roof, "cpu_baseline": cpu}
         if cfg in ("C2", "C4", "C5"):
-            line["pairings_per_s"] = round(world * (leg.units + leg.segments) * args.steps / dt, 1)
+            line["pairings_per_s"] = round((total_units + world * leg.segments) * args.steps / dt, 1)
         if single:
             line["single_batch"] = single
         if getattr(leg, "grouped", None):
             line["config"]["grouped_checks"] = leg.grouped
         if cfg == "C4":
-            line["pks_aggregated_per_s"] = round(world * leg.pks_per_step * args.steps / dt, 1)
+            line["pks_aggregated_per_s"] = round(leg.epoch["keys"] * args.steps / dt, 1)
+            line["epoch"] = dict(leg.epoch, per_committee_check=committee_check)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -29,6 +29,7 @@ if _override:
 # GBLS_INIT_TUNING (include/grandine_bls_gpu.h): tests and sweeps that set the engine's
 # tuning environment variables call enable_tuning() before the first lib() call.
 INIT_TUNING = 0x200
+INIT_PER_CHECK = 0x400  # grouped single checks off (deterministic per-check verdicts)
 _tuning = False
 
 

@@ -35,6 +35,7 @@
 
 #include "../../include/grandine_bls_gpu.h"
 #include "gbls_common.h"
+#include "gbls_sched.h"
 
 using namespace gbls;
 
@@ -49,7 +50,6 @@ namespace {
 
 constexpr int FAILED = GBLS_VERIFY_FAIL;  // engine/driver failure return (fail closed)
 constexpr size_t kShardMinSets = 1024;     // per device, before a batch is split
-constexpr int kMaxCtxPerDevice = 64;
 
 thread_local int t_last_error = GBLS_ERR_NONE;
 
@@ -143,7 +143,7 @@ struct Ctx {
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
   Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, Sj, gpart, lines, Ts, V0, V1, tab, part, err, out0,
-      out1, pks, pre, pre2, msm, sigd, sigst, rnd, ng1, gerr, gv;
+      out1, pks, pre, pre2, msm, sigd, sigst, rnd, ng1, gerr, gv, redo, rtab;
   // per-call option of the next pipeline_partials on this lease: compressed signatures
   // (96 B each, device) to decompress on the signature-side stream into `sigs`, with their
   // BLST_ERROR statuses (device) failing their segments (consumed and reset by the pipeline)
@@ -271,10 +271,7 @@ struct Device {
   int hipdev = -1;
   uint32_t nsimd = 1024;  // 4 SIMDs per CU
   int ncu = 256;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::vector<Ctx *> idle;
-  std::vector<std::unique_ptr<Ctx>> all;
+  sched::CtxPool<Ctx> pool;  // per-class capped context pool (gbls_sched.h)
   Buf reg;  // validator registry (replica), guarded by Engine::reg_mu
 };
 
@@ -286,6 +283,7 @@ struct Engine {
   std::shared_mutex reg_mu;
   size_t reg_n = 0;
   std::atomic<bool> coalesce{true};
+  std::atomic<bool> per_check{false};  // GBLS_INIT_PER_CHECK: no grouped single checks
   size_t msm_min = kMsmMinPerSeg;  // segments at least this large use the bucket MSM
   size_t line_budget = kLineBudget; // line-coefficient buffer bound per submission (bytes)
   uint32_t ml_g = 0;                // forced k_ml_group group size (0: chosen per launch)
@@ -297,40 +295,14 @@ struct Engine {
   int leaders = 2;                  // coalescer leaders per device
 } g;
 
-// RAII lease of a context of one device: the idle context last used on the caller's
-// stream (stream order makes its reuse free), else an idle context whose previous call
-// has finished on the GPU, else a new one (up to kMaxCtxPerDevice), else the least
-// recently used idle context (its reuse is ordered behind its previous call on the GPU)
+// RAII lease of a context of one device (sched::CtxPool::acquire: the idle context last
+// used on the caller's stream, else one idle on the GPU, else a new one up to the class cap,
+// else the least recently used idle one of the class, else wait).
 class Lease {
  public:
   Lease(Device &d, bool affine, hipStream_t stream, int cls = 0) : d_(d) {
-    std::unique_lock<std::mutex> lk(d.mu);
-    for (;;) {
-      for (size_t i = 0; affine && !c_ && i < d.idle.size(); i++)
-        if (d.idle[i]->cls == cls && d.idle[i]->used && d.idle[i]->last_stream == stream) {
-          c_ = d.idle[i];
-          d.idle.erase(d.idle.begin() + i);
-        }
-      for (size_t i = 0; !c_ && i < d.idle.size(); i++)
-        if (d.idle[i]->cls == cls && d.idle[i]->idle_on_gpu()) {
-          c_ = d.idle[i];
-          d.idle.erase(d.idle.begin() + i);
-        }
-      if (!c_ && (int)d.all.size() < kMaxCtxPerDevice) {
-        d.all.emplace_back(new Ctx());
-        c_ = d.all.back().get();
-        fresh_ = true;
-      }
-      for (size_t i = 0; !c_ && i < d.idle.size(); i++)
-        if (d.idle[i]->cls == cls) {
-          c_ = d.idle[i];
-          d.idle.erase(d.idle.begin() + i);
-        }
-      if (c_) break;
-      d.cv.wait(lk);  // every context of this class is leased: wait for one to come back
-    }
-    lk.unlock();
-    ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high, g.prio_mode, cls)
+    c_ = d.pool.acquire(affine, stream, cls, &fresh_);
+    ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high, g.prio_mode, c_->cls)
                  : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
   }
   explicit Lease(Device &d, int cls = 0) : Lease(d, false, nullptr, cls) {}
@@ -342,11 +314,7 @@ class Lease {
       c_->active = false;
       c_->cur = nullptr;
     }
-    {
-      std::lock_guard<std::mutex> lk(d_.mu);
-      d_.idle.push_back(c_);
-    }
-    d_.cv.notify_all();  // waiters of either class
+    d_.pool.release(c_);
   }
   bool ok() const { return ok_; }
   Ctx &operator*() { return *c_; }
@@ -360,6 +328,9 @@ class Lease {
 
 bool engine_init(uint32_t device_mask, uint32_t flags) {
   std::lock_guard<std::mutex> lk(g.mu);
+  // policy flags apply on every call, also to an engine that is already open
+  g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
+  g.per_check.store((flags & GBLS_INIT_PER_CHECK) != 0);
   if (g.ready.load()) return true;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GBLS_ERR_NO_DEVICE);
@@ -373,7 +344,6 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     ids.push_back(cur);
   }
   if (ids.empty()) return fail(GBLS_ERR_NO_DEVICE);
-  g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
   // tuning knobs: only for tests and sweeps that ask for them (GBLS_INIT_TUNING); a node
   // embedding the library runs the measured defaults whatever its environment holds
   if (flags & GBLS_INIT_TUNING) {
@@ -442,12 +412,9 @@ bool valid_offsets(const uint32_t *off, size_t nseg, size_t n) {
   return true;
 }
 
-// ----- where a batch's public keys come from (device pointers inside the pipeline)
-struct PkSource {
-  const g1a *pts = nullptr;       // points: one per set (off == nullptr) or summed per set
-  const uint32_t *idx = nullptr;  // registry indices: one per set (off == nullptr) or summed
-  const uint32_t *off = nullptr;  // per-set ranges [off[i], off[i+1]) of pts / idx
-};
+// ----- where a batch's public keys come from (device pointers inside the pipeline, host
+// pointers in a coalescer request)
+using PkSource = sched::KeySource<g1a>;
 
 // Resolve a DEVICE key source into per-set affine keys on stream st; *pre = per-set
 // status (nonzero = reject: empty aggregate, index out of range) or nullptr.  The caller
@@ -843,15 +810,26 @@ bool fill_random(uint64_t *r, size_t n) {
   return true;
 }
 
+// Round 2 runs entirely on the device (k_groups.hip): k_group_expand writes every check's
+// verdict from its group's and compacts the members to re-check into a list whose length stays
+// on the device; the re-checks then run in fixed passes of R slots (tables, Miller product,
+// Horner step, final exponentiation writing through the list), slots past the count exiting at
+// once.  No host synchronisation: the device entry points stay asynchronous on their stream.
 bool grouped_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *msg_off,
                       const g2a *sigs, const PkSource &src, bool sig_groupcheck, size_t n,
                       const uint32_t *seg_off, int32_t *verdicts, hipStream_t st, bool *done) {
   *done = false;
   const size_t gs = kGroupChecks, ng_max = (n + gs - 1) / gs;
+  // re-check slots per pass: a quarter of the batch (>= 2048); a typical 1 %-invalid batch
+  // re-checks ~8 % of its checks, so one pass does the work and the others exit at once
+  const size_t R = std::min(n, std::max<size_t>(2048, (n + 3) / 4)), passes = (n + R - 1) / R;
   std::vector<uint64_t> r(n);
+  // every buffer sized before round 1, so no growth (and no host wait) happens in between
   if (!fill_random(r.data(), n) || !c.upload_staged(c.rnd, r.data(), n * 8, st) ||
       !c.ensure(c.part, n * sizeof(fp12)) || !c.ensure(c.err, n * sizeof(int32_t) + 16) ||
-      !c.ensure(c.gerr, n * sizeof(int32_t) + 16) || !c.ensure(c.gv, n * sizeof(int32_t) + 16))
+      !c.ensure(c.gerr, n * sizeof(int32_t) + 16) || !c.ensure(c.gv, n * sizeof(int32_t) + 16) ||
+      !c.ensure(c.redo, (n + 16) * sizeof(uint32_t)) || !c.ensure(c.rtab, 5 * R * sizeof(uint32_t)) ||
+      !c.ensure(c.V0, ML_EVENTS * R * sizeof(fp12)))
     return false;
   size_t nms = 0;
   if (!pipeline_partials(c, d, msgs, msg_off, sigs, src, nullptr, sig_groupcheck, n, seg_off, n, 1,
@@ -864,61 +842,30 @@ bool grouped_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *ms
                    c.gerr.as<int32_t>());
   if (!pipeline_final(c.part.as<fp12>(), c.gerr.as<int32_t>(), 1, nms, c.gv.as<int32_t>(), st))
     return false;
-  int32_t *h_gv = static_cast<int32_t *>(c.staging((nms + n) * 4));  // one block: a later
-  if (!h_gv) return fail(GBLS_ERR_HIP);                              // staging() may regrow
-  int32_t *h_err = h_gv + nms;
-  HIPCHK(hipMemcpyAsync(h_gv, c.gv.p, nms * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(h_err, c.err.p, n * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  std::vector<int32_t> out(n, GBLS_VERIFY_FAIL);
-  std::vector<uint32_t> redo;
-  for (size_t gi = 0; gi < nms; gi++) {
-    const size_t b = gi * gs, e = std::min(n, b + gs);
-    bool flagged = false;
-    for (size_t i = b; i < e; i++) flagged |= h_err[i] != 0;
-    const bool pass = !flagged && h_gv[gi] == GBLS_SUCCESS;
-    for (size_t i = b; i < e; i++) {
-      if (pass)
-        out[i] = GBLS_SUCCESS;
-      else if (!h_err[i])
-        redo.push_back((uint32_t)i);  // flagged checks stay GBLS_VERIFY_FAIL
-    }
-  }
-  if (!redo.empty()) {  // round 2: each re-checked member its own Miller segment
-    const size_t m2 = redo.size(), NP = 2 * n;
-    std::vector<uint32_t> &tab = c.host_tab;
-    tab.clear();
-    MlTables mt = ml_tables(
-        tab, m2, 2 * m2, ML_EVENTS, d.nsimd, [](size_t) { return 2u; },
-        [&](size_t s, std::vector<uint32_t> &t) {
-          t.push_back(redo[s]);
-          t.push_back((uint32_t)n + redo[s]);
-        });
-    if (!c.ensure(c.V0, ML_EVENTS * mt.v0_n * sizeof(fp12)) ||
-        !c.ensure(c.V1, ML_EVENTS * mt.v1_n * sizeof(fp12)) ||
-        !c.upload_staged(c.tab, tab.data(), tab.size() * 4, st))
-      return false;
-    const uint32_t *T = c.tab.as<uint32_t>();
+  uint32_t *redo = c.redo.as<uint32_t>(), *cnt = redo + n;
+  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t), st));
+  launch_group_expand(st, c.gv.as<int32_t>(), c.err.as<int32_t>(), (uint32_t)n, (uint32_t)gs, verdicts,
+                      redo, cnt);
+  // round 2: slot j of pass k re-checks redo[k R + j] -- its own Miller product of the SAME
+  // pairs (lines resident since round 1), Horner step and final exponentiation
+  HIPCHK(hipMemsetAsync(c.gerr.p, 0, R * sizeof(int32_t), st));
+  uint32_t *plist = c.rtab.as<uint32_t>(), *grp = plist + 2 * R;
+  for (size_t k = 0; k < passes; k++) {
+    const uint32_t base = (uint32_t)(k * R);
+    launch_redo_tables(st, redo, cnt, base, (uint32_t)R, (uint32_t)n, plist, grp);
     {
       StageTimer t(S_ML_LEAF, st);
-      launch_ml_group(st, c.lines.as<uint32_t>(), (uint32_t)NP, c.P.as<g1s>(), T + mt.plist_off,
-                      T + mt.grp_off, (uint32_t)mt.ngroup, 0, ML_EVENTS, c.V0.as<fp12>());
+      launch_ml_group(st, c.lines.as<uint32_t>(), (uint32_t)(2 * n), c.P.as<g1s>(), plist, grp, (uint32_t)R, 0,
+                      ML_EVENTS, c.V0.as<fp12>());
     }
-    ml_tail(c, st, mt, T, (uint32_t)m2, c.part.as<fp12>());
-    HIPCHK(hipMemsetAsync(c.gerr.p, 0, m2 * 4, st));
-    if (!pipeline_final(c.part.as<fp12>(), c.gerr.as<int32_t>(), 1, m2, c.gv.as<int32_t>(), st))
-      return false;
-    int32_t *h_v2 = static_cast<int32_t *>(c.staging(m2 * 4));
-    if (!h_v2) return fail(GBLS_ERR_HIP);
-    HIPCHK(hipMemcpyAsync(h_v2, c.gv.p, m2 * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    for (size_t k = 0; k < m2; k++) out[redo[k]] = h_v2[k];
+    {
+      StageTimer t(S_ML_HORNER, st);
+      launch_ml_horner(st, c.V0.as<fp12>(), (uint32_t)R, c.part.as<fp12>(), cnt, base);
+    }
+    StageTimer t(S_FINAL, st);
+    launch_final_verdict(st, c.part.as<fp12>(), c.gerr.as<int32_t>(), 1, (uint32_t)R, verdicts, cnt, base, redo);
   }
-  int32_t *h_out = static_cast<int32_t *>(c.staging(n * 4));
-  if (!h_out) return fail(GBLS_ERR_HIP);
-  std::memcpy(h_out, out.data(), n * 4);
-  HIPCHK(hipMemcpyAsync(verdicts, h_out, n * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(hipStreamSynchronize(st));  // h_out is this call's staging memory
+  HIPCHK(hipGetLastError());
   return true;
 }
 
@@ -926,7 +873,8 @@ bool pipeline_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
                        const g2a *sigs, const PkSource &src, const uint64_t *rands,
                        bool sig_groupcheck, size_t n, const uint32_t *seg_off, size_t nseg,
                        int32_t *verdicts, hipStream_t st) {
-  bool ident = !rands && n == nseg && n >= kGroupMinChecks && n <= kGroupMaxChecks;
+  bool ident = !g.per_check.load() && !rands && n == nseg && n >= kGroupMinChecks &&
+               n <= kGroupMaxChecks;
   for (size_t s = 0; ident && s <= nseg; s++) ident = seg_off[s] == s;
   if (ident) {
     bool done = false;
@@ -1042,7 +990,10 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
     size_t k = std::min(ndev, n / kShardMinSets);
     Device &d0 = *g.devs[0];
     Lease L0(d0, cls);
-    if (!L0.ok() || !L0->begin(L0->own)) return false;
+    // L0's part / err become peer-copy destinations of the shard streams, which are not
+    // ordered behind L0's previous call: if the pool handed out a context still busy on the
+    // GPU, wait for that call on the host first (its final step may still read them)
+    if (!L0.ok() || !L0->begin(L0->own) || !L0->drain()) return false;
     hipStream_t st0 = L0->own;
     if (!L0->ensure(L0->part, k * sizeof(fp12)) || !L0->ensure(L0->err, k * 4 + 16) ||
         !L0->ensure(L0->out1, 16))
@@ -1121,175 +1072,22 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
 // key source kind as ONE segmented submission (each request keeps its own segments and
 // verdicts).  Batches therefore grow with the load, while an idle engine runs a lone
 // call immediately (no waiting window).
-// merged gossip submissions stay below one C2 step (~17 ms of GPU time), so a block-import
-// submission never waits long behind one
-constexpr size_t kMaxMergedSets = 1 << 16;
-// collection window of a new leader while another submission is in flight (see below)
-constexpr size_t kMergeTargetSets = 512;
-constexpr int kMergeWindowUs = 300;
-// Block import (GBLS_CALL_BLOCK, transition_functions/src/deneb/state_transition.rs:69-71
-// verifies a block's signatures on the critical path of its import) has its own queue and
-// leader slot per device: it never waits for a normal leader, is merged only with other
-// block requests up to kPrioMaxSets sets (the latency cap), and runs on contexts whose
-// streams all have the highest priority.
-constexpr size_t kPrioMaxSets = 8192;
-
-struct CoReq {
-  const uint8_t *msgs;
-  const g2a *sigs;
-  PkSource src;  // host pointers
-  const uint64_t *rands;
-  size_t n;
-  const uint32_t *seg_off;
-  size_t nseg;
-  int32_t *verdicts;
-  const uint8_t *sigs_c = nullptr;  // compressed signatures instead of sigs (96 B each)
-  int32_t *sig_status = nullptr;    // their decompression statuses (with sigs_c)
-  int prio = 0;                     // 1: block import
-  bool done = false, ok = false;
-  int err = GBLS_ERR_NONE;
-  int kind() const { return (src.pts ? 1 : 0) | (src.off ? 2 : 0) | (sigs_c ? 4 : 0); }
-  size_t nkeys() const { return src.off ? src.off[n] : n; }
-};
-
-struct Coalescer {
-  std::mutex mu;
-  std::condition_variable cv;
-  std::vector<CoReq *> q, pq;  // normal and block-import queues
-  int leaders = 0, pleaders = 0;
-} co;
-
-bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, int32_t *sig_status,
-                 const PkSource &src, const uint64_t *rands, size_t n, const uint32_t *seg_off,
-                 size_t nseg, int32_t *verdicts, int cls);
-
-void run_merged(std::vector<CoReq *> &batch) {
-  if (batch.size() == 1) {
-    CoReq &r = *batch[0];
-    r.ok = verify_host(r.msgs, r.sigs, r.sigs_c, r.sig_status, r.src, r.rands, r.n, r.seg_off,
-                       r.nseg, r.verdicts, r.prio);
-    r.err = t_last_error;
-    return;
-  }
-  size_t n = 0, nseg = 0, nk = 0;
-  for (CoReq *r : batch) {
-    n += r->n;
-    nseg += r->nseg;
-    nk += r->nkeys();
-  }
-  const CoReq &r0 = *batch[0];
-  std::vector<uint8_t> msgs(32 * n), sigc(r0.sigs_c ? 96 * n : 0);
-  std::vector<g2a> sigs(r0.sigs_c ? 0 : n);
-  std::vector<int32_t> sst(r0.sigs_c ? n : 0, GBLS_BAD_ENCODING);
-  std::vector<uint64_t> rands(n);
-  std::vector<g1a> pts;
-  std::vector<uint32_t> idx, off, seg(nseg + 1);
-  if (r0.src.pts) pts.resize(nk);
-  else idx.resize(nk);
-  if (r0.src.off) off.resize(n + 1);
-  std::vector<int32_t> v(nseg, GBLS_VERIFY_FAIL);
-  size_t at = 0, sat = 0, kat = 0;
-  seg[0] = 0;
-  for (CoReq *r : batch) {
-    std::memcpy(&msgs[32 * at], r->msgs, 32 * r->n);
-    if (r0.sigs_c)
-      std::memcpy(&sigc[96 * at], r->sigs_c, 96 * r->n);
-    else
-      std::memcpy(&sigs[at], r->sigs, r->n * sizeof(g2a));
-    std::memcpy(&rands[at], r->rands, r->n * 8);
-    size_t k = r->nkeys();
-    if (r0.src.pts) std::memcpy(&pts[kat], r->src.pts, k * sizeof(g1a));
-    else std::memcpy(&idx[kat], r->src.idx, k * 4);
-    if (r0.src.off)
-      for (size_t i = 0; i <= r->n; i++) off[at + i] = (uint32_t)(kat + r->src.off[i]);
-    for (size_t s = 1; s <= r->nseg; s++) seg[sat + s] = (uint32_t)(at + r->seg_off[s]);
-    at += r->n;
-    sat += r->nseg;
-    kat += k;
-  }
-  PkSource src;
-  if (r0.src.pts) src.pts = pts.data();
-  else src.idx = idx.data();
-  if (r0.src.off) src.off = off.data();
-  bool ok = verify_host(msgs.data(), r0.sigs_c ? nullptr : sigs.data(),
-                        r0.sigs_c ? sigc.data() : nullptr, r0.sigs_c ? sst.data() : nullptr, src,
-                        rands.data(), n, seg.data(), nseg, v.data(), r0.prio);
-  int err = t_last_error;
-  sat = 0;
-  at = 0;
-  for (CoReq *r : batch) {
-    std::memcpy(r->verdicts, &v[sat], r->nseg * 4);
-    if (r0.sigs_c) std::memcpy(r->sig_status, &sst[at], r->n * 4);
-    sat += r->nseg;
-    at += r->n;
-    r->ok = ok;
-    r->err = err;
-  }
-}
+// (gbls_sched.h: queues, leaders, the collection window and the merge itself)
+using CoReq = sched::Request<g1a, g2a>;
+sched::Coalescer<CoReq> co;
 
 bool coalesced_verify(CoReq &r) {
-  if (!g.coalesce.load()) {
-    bool ok = verify_host(r.msgs, r.sigs, r.sigs_c, r.sig_status, r.src, r.rands, r.n, r.seg_off,
-                          r.nseg, r.verdicts, r.prio);
-    return ok;
-  }
-  const int ndev = (int)g.devs.size();
-  const int max_leaders = (r.prio ? 1 : g.leaders) * ndev;
-  const size_t cap = r.prio ? kPrioMaxSets : kMaxMergedSets;
-  std::vector<CoReq *> &q = r.prio ? co.pq : co.q;
-  int &leaders = r.prio ? co.pleaders : co.leaders;
-  std::unique_lock<std::mutex> lk(co.mu);
-  q.push_back(&r);
-  co.cv.notify_all();  // a leader collecting a batch (below) sees the new request at once
-  bool waited = false;
-  while (!r.done) {
-    if (leaders < max_leaders && !q.empty()) {
-      // Another submission is already in flight: the GPU is busy, so a short collection
-      // window costs little latency and lets the callers that return from that submission
-      // join this one (without it the first of them leads a batch of one).  Never for block
-      // import, never on an idle engine.
-      auto queued = [&q]() {
-        size_t t = 0;
-        for (const CoReq *x : q) t += x->n;
-        return t;
-      };
-      if (!r.prio && leaders > 0 && !waited && queued() < kMergeTargetSets) {
-        waited = true;
-        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(kMergeWindowUs);
-        co.cv.wait_until(lk, deadline, [&] { return r.done || queued() >= kMergeTargetSets; });
-        continue;
-      }
-      leaders++;
-      std::vector<CoReq *> batch;
-      auto mine = std::find(q.begin(), q.end(), &r);
-      int kind = mine != q.end() ? r.kind() : q.front()->kind();
-      size_t sets = 0;
-      if (mine != q.end()) {
-        batch.push_back(&r);
-        sets = r.n;
-        q.erase(mine);
-      }
-      for (auto it = q.begin(); it != q.end();) {
-        if ((*it)->kind() == kind && (batch.empty() || sets + (*it)->n <= cap)) {
-          sets += (*it)->n;
-          batch.push_back(*it);
-          it = q.erase(it);
-        } else {
-          ++it;
-        }
-      }
-      lk.unlock();
-      run_merged(batch);  // writes verdicts, ok, err; `done` is published under co.mu
-      lk.lock();
-      for (CoReq *b : batch) b->done = true;
-      leaders--;
-      co.cv.notify_all();
-    } else {
-      co.cv.wait(lk);
-    }
-  }
+  sched::Config cfg;
+  cfg.coalesce = g.coalesce.load();
+  cfg.devices = (int)g.devs.size();
+  cfg.leaders = g.leaders;
+  bool ok = co.submit(r, cfg, [](CoReq &m) {
+    m.ok = verify_host(m.msgs, m.sigs, m.sigs_c, m.sig_status, m.src, m.rands, m.n, m.seg_off,
+                       m.nseg, m.verdicts, m.prio);
+    m.err = t_last_error;  // the leader's thread-local code, handed to every merged caller
+  });
   t_last_error = r.err;
-  return r.ok;
+  return ok;
 }
 
 void fill(int32_t *v, size_t n, int32_t x) {
@@ -1521,6 +1319,7 @@ int gbls_g1_aggregate_indexed(const uint32_t *idx, const uint32_t *seg_offsets, 
 }
 
 int gbls_g1_aggregate(const gbls_p1_affine *pks, size_t n, gbls_p1_affine *out) {
+  t_last_error = GBLS_ERR_NONE;
   uint32_t off[2] = {0, (uint32_t)n};
   int32_t st = GBLS_AGGR_TYPE_MISMATCH;
   if (n == 0) {
@@ -1532,6 +1331,7 @@ int gbls_g1_aggregate(const gbls_p1_affine *pks, size_t n, gbls_p1_affine *out) 
 }
 
 int gbls_g2_aggregate(const gbls_p2_affine *sigs, size_t n, gbls_p2_affine *out) {
+  t_last_error = GBLS_ERR_NONE;
   uint32_t off[2] = {0, (uint32_t)n};
   int32_t st = GBLS_AGGR_TYPE_MISMATCH;
   if (n == 0) {
@@ -1620,6 +1420,7 @@ int gbls_fast_aggregate_verify_indexed(const gbls_p2_affine *sigs, const uint8_t
 
 int gbls_fast_aggregate_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
                                const gbls_p1_affine *pks, size_t n) {
+  t_last_error = GBLS_ERR_NONE;
   if (n == 0) return GBLS_VERIFY_FAIL;  // blst: AGGR_TYPE_MISMATCH -> not SUCCESS
   uint32_t moff[2] = {0, (uint32_t)msg_len};
   uint32_t soff[2] = {0, (uint32_t)n};
@@ -1650,6 +1451,7 @@ int gbls_multi_verify_segments(const uint8_t (*msgs)[32], const gbls_p2_affine *
 
 int gbls_multi_verify(const uint8_t (*msgs)[32], const gbls_p2_affine *sigs,
                       const gbls_p1_affine *pks, const uint64_t *rands, size_t n) {
+  t_last_error = GBLS_ERR_NONE;  // the early verdicts below are verdicts, not engine errors
   if (n == 0) return GBLS_VERIFY_FAIL;
   for (size_t i = 0; i < n; i++)
     if (rands[i] == 0) return GBLS_VERIFY_FAIL;  // NonZeroU64 contract
@@ -1679,6 +1481,7 @@ int gbls_multi_verify_compressed_ex(const uint8_t (*msgs)[32], const uint8_t (*s
                                     const gbls_p1_affine *pks, const uint32_t *pk_idx,
                                     const uint32_t *pk_off, const uint64_t *rands, size_t n,
                                     int32_t *sig_status, uint32_t call_flags) {
+  t_last_error = GBLS_ERR_NONE;
   if (!sig_status) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
   fill(sig_status, n, GBLS_BAD_ENCODING);
   API_BEGIN

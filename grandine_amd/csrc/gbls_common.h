@@ -129,10 +129,22 @@ void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g
                      int e1, fp12 *V0);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);
-void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial);
+// lim (device count, optional): only segments s with base + s < *lim run (the others exit)
+void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial,
+                      const uint32_t *lim = nullptr, uint32_t base = 0);
 
 // k_fexp.hip -- product of partials, final exponentiation, verdict
+// lim / base as in launch_ml_horner; scatter (optional): segment s's verdict goes to
+// verdict[scatter[base + s]] instead of verdict[s]
 void launch_final_verdict(hipStream_t st, const fp12 *partials, const int32_t *err,
-                          uint32_t nparts, uint32_t nseg, int32_t *verdict);
+                          uint32_t nparts, uint32_t nseg, int32_t *verdict,
+                          const uint32_t *lim = nullptr, uint32_t base = 0,
+                          const uint32_t *scatter = nullptr);
+
+// k_groups.hip -- second round of the grouped single checks, on the device
+void launch_group_expand(hipStream_t st, const int32_t *gv, const int32_t *err, uint32_t n, uint32_t gs,
+                         int32_t *verdicts, uint32_t *redo, uint32_t *cnt);
+void launch_redo_tables(hipStream_t st, const uint32_t *redo, const uint32_t *cnt, uint32_t base, uint32_t R,
+                        uint32_t n, uint32_t *plist, uint32_t *grp);
 
 }  // namespace gbls

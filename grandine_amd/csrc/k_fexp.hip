@@ -19,14 +19,16 @@ namespace gbls {
 // are generic Fp12 squarings (G is not in the cyclotomic subgroup).
 __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const int32_t *err,
                                                       uint32_t nparts, uint32_t nseg,
-                                                      int32_t *verdict) {
+                                                      int32_t *verdict, const uint32_t *lim,
+                                                      uint32_t base, const uint32_t *scatter) {
   W12_SHARED uint32_t f[W12_WORDS], G[W12_WORDS], A[W12_WORDS], B[W12_WORDS], T[W12_WORDS],
       X[W12_WORDS], ws[W12_WS_WORDS];
   __shared__ int bad;
   int lane = threadIdx.x;
+  uint32_t s = blockIdx.x;
+  if (lim && base + s >= *lim) return;  // block-uniform
   w12_plan pl;
   w12_begin(pl, ws);
-  uint32_t s = blockIdx.x;
   const uint32_t *src = reinterpret_cast<const uint32_t *>(part + s);
   for (int i = lane; i < W12_WORDS; i += 64) f[i] = src[i];
   if (lane == 0) bad = err[s];
@@ -64,7 +66,8 @@ __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const in
   w12_mul(pl, X, G, G, ws);
   w12_mul(pl, X, X, G, ws);
   w12_mul(pl, A, A, X, ws);
-  if (lane == 0) verdict[s] = (!bad && w12_is_fp6_image(A)) ? ST_SUCCESS : ST_VERIFY_FAIL;
+  if (lane == 0)
+    verdict[scatter ? scatter[base + s] : s] = (!bad && w12_is_fp6_image(A)) ? ST_SUCCESS : ST_VERIFY_FAIL;
 }
 
 // The same verdict on the row-distributed Fp12 engine (bls_w12d.h): one 56-row workgroup per
@@ -75,14 +78,16 @@ __global__ void __launch_bounds__(64) k_final_verdict(const fp12 *part, const in
 __global__ void __launch_bounds__(w12d::THREADS) k_final_verdict_d(const fp12 *part,
                                                                    const int32_t *err,
                                                                    uint32_t nparts, uint32_t nseg,
-                                                                   int32_t *verdict) {
+                                                                   int32_t *verdict, const uint32_t *lim,
+                                                                   uint32_t base, const uint32_t *scatter) {
   __shared__ __attribute__((aligned(16))) uint32_t f[w12d::IMG], G[w12d::IMG], A[w12d::IMG],
       B[w12d::IMG], T[w12d::IMG], X[w12d::IMG], ws[w12d::WS];
   __shared__ int flags[12];
   __shared__ int bad;
+  const uint32_t s = blockIdx.x;
+  if (lim && base + s >= *lim) return;  // block-uniform
   w12d::Eng e;
   w12d::begin(e, ws);
-  const uint32_t s = blockIdx.x;
   w12d::load_scaled(e, f, reinterpret_cast<const uint32_t *>(part + s));
   if (threadIdx.x == 0) bad = err[s];
   for (uint32_t k2 = 1; k2 < nparts; k2++) {
@@ -122,7 +127,7 @@ __global__ void __launch_bounds__(w12d::THREADS) k_final_verdict_d(const fp12 *p
   if (threadIdx.x == 0) {
     int fp6 = 1;
     for (int i = 6; i < 12; i++) fp6 &= flags[i];
-    verdict[s] = (!bad && fp6) ? ST_SUCCESS : ST_VERIFY_FAIL;
+    verdict[scatter ? scatter[base + s] : s] = (!bad && fp6) ? ST_SUCCESS : ST_VERIFY_FAIL;
   }
 }
 
@@ -130,12 +135,14 @@ __global__ void __launch_bounds__(w12d::THREADS) k_final_verdict_d(const fp12 *p
 constexpr uint32_t kFinalRowsMaxSegs = 64;
 
 void launch_final_verdict(hipStream_t st, const fp12 *partials, const int32_t *err,
-                          uint32_t nparts, uint32_t nseg, int32_t *verdict) {
+                          uint32_t nparts, uint32_t nseg, int32_t *verdict, const uint32_t *lim,
+                          uint32_t base, const uint32_t *scatter) {
   if (!nseg) return;
   if (nseg <= kFinalRowsMaxSegs)
-    k_final_verdict_d<<<nseg, w12d::THREADS, 0, st>>>(partials, err, nparts, nseg, verdict);
+    k_final_verdict_d<<<nseg, w12d::THREADS, 0, st>>>(partials, err, nparts, nseg, verdict, lim, base,
+                                                       scatter);
   else
-    k_final_verdict<<<nseg, 64, 0, st>>>(partials, err, nparts, nseg, verdict);
+    k_final_verdict<<<nseg, 64, 0, st>>>(partials, err, nparts, nseg, verdict, lim, base, scatter);
 }
 
 }  // namespace gbls

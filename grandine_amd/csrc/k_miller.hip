@@ -121,11 +121,13 @@ __global__ void __launch_bounds__(64) k_ml_reduce(const fp12 *Vin, uint32_t nin,
 }
 
 // grid nseg: V holds one value per (event, segment): V[e * nseg + s]
-__global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, fp12 *partial) {
+__global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, fp12 *partial,
+                                                  const uint32_t *lim, uint32_t base) {
   W12_SHARED uint32_t acc[W12_WORDS], tmp[W12_WORDS], ws[W12_WS_WORDS];
+  uint32_t s = blockIdx.x;
+  if (lim && base + s >= *lim) return;  // block-uniform
   w12_plan pl;
   w12_begin(pl, ws);
-  uint32_t s = blockIdx.x;
   w12_load(acc, V + s);
   for (int e = 1; e < ML_EVENTS; e++) {
     if (ev_is_dbl(e)) w12_mul(pl, acc, acc, acc, ws);
@@ -160,12 +162,14 @@ void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint3
 // limbs (an Fp* scalar each; the final exponentiation removes them); the partial is written
 // as canonical engine-form words.
 __global__ void __launch_bounds__(w12d::THREADS) k_ml_horner_d(const fp12 *V, uint32_t nseg,
-                                                               fp12 *partial) {
+                                                               fp12 *partial, const uint32_t *lim,
+                                                               uint32_t base) {
   __shared__ __attribute__((aligned(16))) uint32_t ev[ML_EVENTS * w12d::IMG], acc[w12d::IMG],
       ws[w12d::WS];
+  const uint32_t s = blockIdx.x;
+  if (lim && base + s >= *lim) return;  // block-uniform
   w12d::Eng e;
   w12d::begin(e, ws);
-  const uint32_t s = blockIdx.x;
   for (uint32_t q = e.row; q < (uint32_t)ML_EVENTS * 12; q += w12d::ROWS) {
     const uint32_t ev_i = q / 12, c = q % 12;
     const uint32_t *w = reinterpret_cast<const uint32_t *>(V + (size_t)ev_i * nseg + s) + 12 * c;
@@ -184,12 +188,13 @@ __global__ void __launch_bounds__(w12d::THREADS) k_ml_horner_d(const fp12 *V, ui
 // segments up to this many take the row-distributed (latency) form
 constexpr uint32_t kHornerRowsMaxSegs = 64;
 
-void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial) {
+void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial,
+                      const uint32_t *lim, uint32_t base) {
   if (!nseg) return;
   if (nseg <= kHornerRowsMaxSegs)
-    k_ml_horner_d<<<nseg, w12d::THREADS, 0, st>>>(V, nseg, partial);
+    k_ml_horner_d<<<nseg, w12d::THREADS, 0, st>>>(V, nseg, partial, lim, base);
   else
-    k_ml_horner<<<nseg, 64, 0, st>>>(V, nseg, partial);
+    k_ml_horner<<<nseg, 64, 0, st>>>(V, nseg, partial, lim, base);
 }
 
 }  // namespace gbls

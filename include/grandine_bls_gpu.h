@@ -112,9 +112,15 @@ enum {
  * GBLS_INIT_TUNING (tests and benchmark sweeps only) lets gbls_init read the engine's
  * tuning environment variables (GBLS_MSM_MIN, GBLS_LINE_BUDGET_MB, GBLS_ML_G,
  * GBLS_ML_ROUNDS, GBLS_PRIO_MODE, GBLS_SIDE2_HIGH, GBLS_ROW_CLEAR_MAX); without it the
- * measured defaults are fixed and no environment variable changes the engine. */
+ * measured defaults are fixed and no environment variable changes the engine.
+ * GBLS_INIT_PER_CHECK: batches of independent checks get one Miller product and final
+ * exponentiation per check (deterministic, as the reference's fast_aggregate_verify) instead
+ * of the grouped form described at gbls_fast_aggregate_verify_batch.
+ * The policy flags (GBLS_INIT_NO_COALESCE, GBLS_INIT_PER_CHECK) take effect on every
+ * gbls_init call, also on an engine that is already open; the other bits only on the first. */
 #define GBLS_INIT_NO_COALESCE 0x100u
 #define GBLS_INIT_TUNING 0x200u
+#define GBLS_INIT_PER_CHECK 0x400u
 int gbls_init(uint32_t device_mask, uint32_t flags);
 int gbls_last_error(void);
 const char *gbls_version(void);
@@ -157,7 +163,19 @@ int gbls_fast_aggregate_verify(const gbls_p2_affine *sig, const uint8_t *msg, si
 int gbls_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                 const uint32_t *msg_off, const gbls_p1_affine *pks, size_t m,
                                 int32_t *verdicts);
-/* C3 shape: m fast_aggregate_verify calls, pks of message i = pks[seg_off[i] .. seg_off[i+1]) */
+/* C3 shape: m fast_aggregate_verify calls, pks of message i = pks[seg_off[i] .. seg_off[i+1]).
+ *
+ * Grouped verdicts (batches of 2048..65536 independent checks: gbls_aggregate_verify_batch,
+ * gbls_fast_aggregate_verify_batch / _indexed / _indexed_device).  Each check i is weighted by
+ * a secret random 64-bit r_i drawn from getrandom(2) on every call, and 8 consecutive checks
+ * share ONE Miller product and final exponentiation: prod_i (e(pk_i, H_i) e(-g1, sig_i))^r_i.
+ * A group whose check passes gives SUCCESS to all its members; every member of a failed group
+ * is re-checked on its own (deterministically: its own pairing product of the same pairs).
+ * So a verdict can differ from the reference's deterministic check (signature.rs:77-93) only
+ * when an invalid check sits in a group that passes, which happens with probability <= 2^-64
+ * per group over the r_i (the random-linear-combination soundness of Signature::multi_verify,
+ * signature.rs:95-129); a valid check is never rejected.  GBLS_INIT_PER_CHECK turns grouping
+ * off (e.g. for spec tests). */
 int gbls_fast_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                      const uint32_t *msg_off, const gbls_p1_affine *pks,
                                      const uint32_t *seg_off, size_t m, int32_t *verdicts);

@@ -47,6 +47,7 @@ pub const GBLS_ERR_ARG: c_int = 102;
 // gbls_init flags
 pub const GBLS_INIT_NO_COALESCE: u32 = 0x100;
 pub const GBLS_INIT_TUNING: u32 = 0x200;
+pub const GBLS_INIT_PER_CHECK: u32 = 0x400;
 // gbls_multi_verify_compressed_ex call flags
 pub const GBLS_CALL_BLOCK: u32 = 0x1;
 

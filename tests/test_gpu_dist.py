@@ -44,3 +44,18 @@ def test_bench_two_rank_c2_leg():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0, line
+
+
+def test_bench_two_rank_c4_epoch_strong_scaling():
+    """VERDICT r03 "next 6": C4 as BASELINE.json configs[3] names it -- ONE mainnet epoch (2048
+    committees over a 2^20-key registry) split into whole committees per rank (1024 each), the
+    ranks' Miller partials all-gathered into one final exponentiation, strong scaling; the bench
+    then checks every committee's own verdict on its rank and sums them over the ranks."""
+    r = _run([os.path.join(ROOT, "bench.py"), "--config", "C4", "--gpus", "2", "--steps", "2", "--warmup", "1",
+              "--no-cpu"], 600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0, line
+    assert line["epoch"]["committees"] == 2048 and line["epoch"]["keys"] == (1 << 20) - 576, line
+    assert line["epoch"]["per_committee_check"] == {"committees_verified": 2048, "committees": 2048}, line
+    assert line["config"]["units_per_gpu_per_step"] == 1024, line

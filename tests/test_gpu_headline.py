@@ -237,6 +237,25 @@ def test_fast_aggregate_verify_grouped_matches_single_checks(G, L, F):
                 keys.append(raw)
         key_l[i] = keys
         expect[i] = c["expect"]
+    # two checks in ONE group whose UNWEIGHTED pairing products cancel -- same key
+    # and message, signatures sigma + D and sigma - D (D in G2).  Each is invalid, but their
+    # product e(pk, H)^2 e(-g1, 2 sigma) is 1, so only the secret r_i weights (on both G1 sides
+    # of each check) can make the group fail
+    P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+
+    def neg(pt):  # affine G2 point, Montgomery bytes: y -> p - y per Fp component
+        y0, y1 = (int.from_bytes(pt[96 + 48 * k:144 + 48 * k], "little") for k in range(2))
+        return pt[:96] + b"".join(((P - y) % P).to_bytes(48, "little") for y in (y0, y1))
+
+    def add(a, b):
+        out = ctypes.create_string_buffer(192)
+        G.check(L.gbls_g2_aggregate(G.buf(a + b), 2, out), "g2 sum")
+        return out.raw
+
+    D, sigma = sig_l[5], sig_l[16]
+    sig_l[16], sig_l[17] = add(sigma, D), add(sigma, neg(D))
+    msg_l[17], key_l[17] = msg_l[16], key_l[16]
+    expect[16] = expect[17] = False
 
     def run(b, e):
         moff, koff, keys = [0], [0], []
@@ -256,3 +275,62 @@ def test_fast_aggregate_verify_grouped_matches_single_checks(G, L, F):
         single += run(b, b + 1024)
     assert grouped == single
     assert [x == G.SUCCESS for x in grouped] == expect
+    assert grouped[16] == grouped[17] == G.VERIFY_FAIL  # the cancelling pair
+    # GBLS_INIT_PER_CHECK: the same 4096-check batch in ONE call with
+    # grouping off (a Miller product and final exponentiation per check) -> the same verdicts
+    PER_CHECK = 0x400
+    assert L.gbls_init(0, PER_CHECK) == G.SUCCESS
+    try:
+        per_check = run(0, n)
+    finally:
+        assert L.gbls_init(0, 0) == G.SUCCESS
+    assert per_check == grouped
+
+
+def test_grouped_device_call_is_asynchronous(G, L, F):
+    """the grouped form's second round (member verdicts, re-checks of
+    failed groups) runs on the device, so gbls_fast_aggregate_verify_indexed_device returns
+    before its stream has finished, and its verdicts (checked after the stream sync) are right:
+    4096 sync-committee-shaped checks over registry indices, 1 % invalid."""
+    import numpy as np
+    import time
+    import torch
+    dev = torch.device("cuda", 0)
+    k, m = 64, 4096
+    sks, comp = F.registry(1 << 12, seed=b"async-fav")
+    first = G.lib().gbls_registry_size()
+    assert not F.load_registry(comp, first).any()
+    rng = np.random.default_rng(11)
+    committee = rng.choice(1 << 12, size=k, replace=False).astype(np.uint32)
+    ssum = sum(sks[int(i)] for i in committee) % F.R_ORDER
+    msgs = F.messages(m, b"async-fav")
+    sigs = bytearray(F.sign([ssum] * m, msgs))
+    bad = sorted(rng.choice(m, size=m // 100, replace=False).tolist())
+    wrong = F.sign([(ssum + 1) % F.R_ORDER], msgs[:32])
+    for i in bad:
+        sigs[192 * i:192 * i + 192] = wrong
+    d_msgs = torch.frombuffer(bytearray(msgs), dtype=torch.uint8).to(dev)
+    d_sigs = torch.frombuffer(sigs, dtype=torch.uint8).to(dev)
+    d_idx = torch.from_numpy((np.tile(committee, m) + first).astype(np.uint32).view(np.int32)).to(dev)
+    d_off = torch.from_numpy(np.arange(0, k * m + 1, k, dtype=np.uint32).view(np.int32)).to(dev)
+    d_v = torch.full((m,), -1, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream()
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    with torch.cuda.stream(s):
+        # warm (buffers grown), then the measured call
+        G.check(L.gbls_fast_aggregate_verify_indexed_device(ptr(d_sigs), ptr(d_msgs), ptr(d_idx), ptr(d_off), m,
+                                                            ptr(d_v), ctypes.c_void_p(s.cuda_stream)), "warm")
+        s.synchronize()
+        d_v.fill_(-1)
+        t0 = time.perf_counter()
+        G.check(L.gbls_fast_aggregate_verify_indexed_device(ptr(d_sigs), ptr(d_msgs), ptr(d_idx), ptr(d_off), m,
+                                                            ptr(d_v), ctypes.c_void_p(s.cuda_stream)), "fav")
+        t_call = time.perf_counter() - t0
+        pending = not s.query()
+        s.synchronize()
+        t_all = time.perf_counter() - t0
+    assert pending, "the device call returned after its stream had finished (host-synchronous)"
+    want = np.zeros(m, dtype=np.int32)
+    want[bad] = G.VERIFY_FAIL
+    assert (d_v.cpu().numpy() == want).all()
+    assert t_call < t_all, (t_call, t_all)
