@@ -209,19 +209,23 @@ HD void jac_add_aff(jac<F> &r, const jac<F> &a, const aff<F> &b) {
   f_sub(r.y, t, u2);     // Y3 = r (V - X3) - 2 Y1 J
 }
 
+// No early return for infinity: Z = 0 inverts to 0 (fp_inv's loop ends at once) and the
+// result is then zeroed by a select, so the point at infinity maps to (0, 0), the all-zero
+// affine encoding.  (The early return made the compiler keep the output in scratch memory:
+// 92 B per lane in every G2 kernel that ends with an affine conversion.)
 template <class F>
 HD void jac_to_aff(aff<F> &r, const jac<F> &p) {
-  if (jac_is_inf(p)) {
-    f_zero(r.x);
-    f_zero(r.y);
-    return;
-  }
+  const bool inf = jac_is_inf(p);
   F zi, zi2, zi3;
   f_inv(zi, p.z);
   f_sqr(zi2, zi);
   f_mul(zi3, zi2, zi);
   f_mul(r.x, p.x, zi2);
   f_mul(r.y, p.y, zi3);
+  if (inf) {
+    f_zero(r.x);
+    f_zero(r.y);
+  }
 }
 
 // Jacobian equality without inversion: X1 Z2^2 == X2 Z1^2 and Y1 Z2^3 == Y2 Z1^3

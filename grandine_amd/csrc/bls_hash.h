@@ -373,10 +373,9 @@ HD void iso_map_g2(g2j &out, const g2j &in) {
   fp2_mul(t, fp2_const(k::ISO_YDEN1_C0, k::ISO_YDEN1_C1), x);
   fp2_add(yd, yd, t);
   fp2_add(yd, yd, fp2_const(k::ISO_YDEN0_C0, k::ISO_YDEN0_C1));
-  if (fp2_is_zero(xd) || fp2_is_zero(yd)) {  // exceptional: image is the identity
-    jac_set_inf(out);
-    return;
-  }
+  // exceptional (xd or yd zero): the image is the identity, selected after the arithmetic
+  // (an early return made the compiler keep the output in scratch memory)
+  const bool exc = fp2_is_zero(xd) || fp2_is_zero(yd);
   fp2 yd2, xd3;
   fp2_sqr(yd2, yd);
   fp2_mul(out.x, xn, xd);
@@ -387,6 +386,7 @@ HD void iso_map_g2(g2j &out, const g2j &in) {
   fp2_mul(t, t, xd3);
   fp2_mul(out.y, t, yd2);
   fp2_mul(out.z, xd, yd);
+  if (exc) jac_set_inf(out);
 }
 
 // h_eff P = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P)  (Budroni-Pintore; RFC 9380 G.3):

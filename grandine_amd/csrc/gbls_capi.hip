@@ -134,6 +134,9 @@ struct Ctx {
   // latency-regime streams on disjoint CU sets (created on first use, see cu_split): the
   // main chain's waves never share a SIMD with the side streams' waves
   hipStream_t own_m = nullptr, side1_m = nullptr, side2_m = nullptr;
+  // normal-class streams kept off the CUs reserved for block import while a block is being
+  // verified (created on first use, see Engine::block_reserve)
+  hipStream_t own_g = nullptr, side1_g = nullptr, side2_g = nullptr;
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
              ev_done = nullptr, ev_upl = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool done_pending = false, upl_pending = false;
@@ -191,6 +194,18 @@ struct Ctx {
     HIPCHK(hipExtStreamCreateWithCUMask(&own_m, (uint32_t)mm.size(), mm.data()));
     HIPCHK(hipExtStreamCreateWithCUMask(&side1_m, (uint32_t)ms.size(), ms.data()));
     HIPCHK(hipExtStreamCreateWithCUMask(&side2_m, (uint32_t)ms.size(), ms.data()));
+    return true;
+  }
+  // streams on every CU except one in `reserve` (CU i with i % reserve == reserve - 1): a normal
+  // submission's kernels cannot occupy those, so a block import's waves always find SIMDs there
+  bool init_gossip_masked(int reserve, int ncu) {
+    if (own_g) return true;
+    std::vector<uint32_t> m((ncu + 31) / 32, 0);
+    for (int i = 0; i < ncu; i++)
+      if (i % reserve != reserve - 1) m[i / 32] |= 1u << (i % 32);
+    HIPCHK(hipExtStreamCreateWithCUMask(&own_g, (uint32_t)m.size(), m.data()));
+    HIPCHK(hipExtStreamCreateWithCUMask(&side1_g, (uint32_t)m.size(), m.data()));
+    HIPCHK(hipExtStreamCreateWithCUMask(&side2_g, (uint32_t)m.size(), m.data()));
     return true;
   }
   // the call's main stream waits (on the GPU) for the previous call on this context;
@@ -293,6 +308,11 @@ struct Engine {
   int cu_split = 0;                 // latency-regime submissions on CU-masked streams (0: off)
   uint32_t cu_split_max = 1024;     // ... up to this many sets
   int leaders = 2;                  // coalescer leaders per device
+  // Block import under load (f3): while a GBLS_CALL_BLOCK call is in progress, normal-class
+  // submissions run on streams masked off one CU in block_reserve (0: off), so the block's
+  // waves never wait for SIMDs held by gossip kernels launched meanwhile.
+  int block_reserve = 4;
+  std::atomic<int> block_active{0};
 } g;
 
 // RAII lease of a context of one device (sched::CtxPool::acquire: the idle context last
@@ -361,6 +381,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_CU_SPLIT_MAX"))
       g.cu_split_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LEADERS")) g.leaders = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("GBLS_BLOCK_RESERVE")) g.block_reserve = std::atoi(e);
 #ifdef GBLS_EXPERIMENTS
     if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
 #endif
@@ -566,6 +587,11 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     own = c.own_m;
     side1 = c.side1_m;
     side2 = c.side2_m;
+  } else if (c.cls == 0 && g.block_reserve > 1 && g.block_active.load(std::memory_order_relaxed) > 0) {
+    if (!c.init_gossip_masked(g.block_reserve, d.ncu)) return false;
+    own = c.own_g;
+    side1 = c.side1_g;
+    side2 = c.side2_g;
   }
   hipStream_t st = caller;
   if (caller != own) {
@@ -1497,6 +1523,15 @@ int gbls_multi_verify_compressed_ex(const uint8_t (*msgs)[32], const uint8_t (*s
   r.sigs_c = &sigs[0][0];
   r.sig_status = sig_status;
   r.prio = (call_flags & GBLS_CALL_BLOCK) ? 1 : 0;
+  struct BlockActive {  // normal submissions keep off the reserved CUs meanwhile
+    bool on;
+    explicit BlockActive(bool b) : on(b) {
+      if (on) g.block_active.fetch_add(1);
+    }
+    ~BlockActive() {
+      if (on) g.block_active.fetch_sub(1);
+    }
+  } block_active(r.prio != 0);
   if (!coalesced_verify(r)) {
     fill(sig_status, n, GBLS_BAD_ENCODING);
     return GBLS_VERIFY_FAIL;

@@ -93,6 +93,62 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n,
   H[i] = o;
 }
 
+// The lane form in two kernels, one [|x|] chain each: in one kernel P and
+// t1 = [x]P stay live through the second chain next to its base and accumulator, and the
+// kernel spilled 100 B per lane; here each chain holds only its base, its accumulator and the
+// addition's temporaries, and the points between the chains wait in the message's own two Q
+// slots in HBM (576 B per message).  The same group element as clear_cofactor_g2 (RFC 9380
+// G.3 order, as clear_cofactor28_parked):
+//   a: P = Q0 + Q1;  t1 = [x]P;  t2 = t1 + psi(P) -> Q[2i];  T = psi^2(2P) - psi(P) - P - t1 -> Q[2i+1]
+//   b: h = [x] t2 + T -> affine H[i]
+__global__ void __launch_bounds__(WG) k_h2c_clear_lane_a(g2j *Q, uint32_t n) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g2j p = Q[2 * i], t1;
+  {
+    const g2j q1 = Q[2 * i + 1];
+    jac_add(p, p, q1);
+  }
+  mul_by_xabs(t1, p);
+  jac_neg(t1, t1);  // t1 = [x]P
+  {
+    g2j t2;
+    g2_psi(t2, p);
+    jac_add(t2, t2, t1);  // t2 = t1 + psi(P)
+    Q[2 * i] = t2;
+  }
+  jac_neg(t1, t1);  // -t1
+  {
+    g2j v;
+    jac_neg(v, p);
+    jac_add(t1, t1, v);  // - t1 - P
+    jac_dbl(v, p);
+    g2_psi2(v, v);
+    jac_add(t1, t1, v);  // + psi^2(2P)
+    g2_psi(v, p);
+    jac_neg(v, v);
+    jac_add(t1, t1, v);  // - psi(P)
+  }
+  Q[2 * i + 1] = t1;
+}
+__global__ void __launch_bounds__(WG) k_h2c_clear_lane_b(const g2j *Q, uint32_t n, g2a *H) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  g2j h;
+  {
+    const g2j t2 = Q[2 * i];
+    mul_by_xabs(h, t2);
+  }
+  jac_neg(h, h);  // [x] t2
+  {
+    const g2j T = Q[2 * i + 1];
+    jac_add(h, h, T);
+  }
+  g2a o;
+  jac_to_aff(o, h);
+  H[i] = o;
+}
+
 // one wave per message (bls_w4.h: four row-distributed products per round), the smallest
 // launches: Q0 + Q1, the cofactor clearing and the affine conversion at ~0.5 us per round
 template <bool X>
@@ -178,8 +234,12 @@ void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
 #endif
   if (n <= kW4Max)
     (n <= w4::kExclusiveMaxWaves ? k_h2c_clear_w4<true> : k_h2c_clear_w4<false>)<<<n, 64, 0, st>>>(Q, n, H);
-  else if (n >= kLaneRegimeClear)
-    k_h2c_clear_lane<<<nblk(n), WG, 0, st>>>(Q, n, H);
+  else if (n >= kLaneRegimeClear) {
+    // Q is a scratch of the call (the map's output); its two slots per message carry the
+    // points between the two chains
+    k_h2c_clear_lane_a<<<nblk(n), WG, 0, st>>>(const_cast<g2j *>(Q), n);
+    k_h2c_clear_lane_b<<<nblk(n), WG, 0, st>>>(Q, n, H);
+  }
   else if (n <= g_row_clear_max)
     k_h2c_clear_row<<<nblk((size_t)n * 16), WG, 0, st>>>(Q, n, H);
   else

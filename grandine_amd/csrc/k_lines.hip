@@ -106,6 +106,81 @@ __global__ void __launch_bounds__(WG) k_lines_row(const g2a *H, uint32_t first, 
   if (e1 < ML_EVENTS && l == 0) Ts[pair] = T;
 }
 
+// The lane regime's line steps (bls_pairing.h line_dbl / line_add_aff, the same operations on
+// the same operands, so the same values) reordered so that each line coefficient is stored as
+// soon as it is known: the three Fp2 coefficients (72 registers) are never live together with
+// the step's temporaries, which kept k_lines_lane spilling 196 B per lane.
+__device__ __forceinline__ void put_fp2(uint32_t *L, uint32_t np, uint32_t pair, int e, int c, const fp2 &v) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) L[line_word(e, c, i, np, pair)] = v.c0.l[i];
+#pragma unroll
+  for (int i = 0; i < 12; i++) L[line_word(e, c + 1, i, np, pair)] = v.c1.l[i];
+}
+__device__ __forceinline__ void lane_line_dbl(g2h &T, uint32_t *L, uint32_t np, uint32_t pair, int e) {
+  fp2 A, B, E, H, t;
+  fp2_sqr(B, T.y);       // Y^2
+  fp2_sqr(t, T.z);       // C = Z^2
+  fp2_mul_3b(E, t);      // 3b'Z^2
+  fp2_add(H, T.y, T.z);
+  fp2_sqr(H, H);
+  fp2_sub(H, H, B);
+  fp2_sub(H, H, t);      // 2YZ                      (C dead)
+  fp2_mul(A, T.x, T.y);
+  fp2_half(A, A);        // XY/2                     (Y dead)
+  fp2_neg(t, H);
+  put_fp2(L, np, pair, e, 4, t);  // L3 = -2YZ
+  fp2_sub(t, E, B);
+  put_fp2(L, np, pair, e, 0, t);  // L0 = 3b'Z^2 - Y^2
+  fp2_sqr(t, T.x);
+  fp2_mul3(t, t);
+  put_fp2(L, np, pair, e, 2, t);  // L2 = 3X^2          (X dead)
+  fp2 F;
+  fp2_add(F, E, E);
+  fp2_add(F, F, E);      // 3E
+  fp2_sub(t, B, F);
+  fp2_mul(T.x, A, t);    // X3 = A (B - F)          (A dead)
+  fp2_mul(T.z, B, H);    // Z3 = B H                (H dead)
+  fp2_add(t, B, F);
+  fp2_half(t, t);
+  fp2_sqr(t, t);         // G^2
+  fp2_sqr(E, E);
+  fp2_mul3(E, E);        // 3E^2
+  fp2_sub(T.y, t, E);    // Y3 = G^2 - 3E^2
+}
+__device__ __forceinline__ void lane_line_add_aff(g2h &T, const g2a &Q, uint32_t *L, uint32_t np, uint32_t pair,
+                                                  int e) {
+  fp2 th, la, t, u;
+  fp2_mul(t, Q.y, T.z);
+  fp2_sub(th, T.y, t);
+  fp2_mul(t, Q.x, T.z);
+  fp2_sub(la, T.x, t);
+  fp2_mul(u, th, Q.x);
+  fp2_mul(t, la, Q.y);
+  fp2_sub(u, u, t);
+  put_fp2(L, np, pair, e, 0, u);   // L0 = theta x2 - lambda y2
+  fp2_neg(u, th);
+  put_fp2(L, np, pair, e, 2, u);   // L2 = -theta
+  put_fp2(L, np, pair, e, 4, la);  // L3 = lambda
+  fp2 vv, vvv, R, A;
+  fp2_sqr(u, th);                  // uu
+  fp2_sqr(vv, la);
+  fp2_mul(vvv, vv, la);
+  fp2_neg(vvv, vvv);       // v^3 = -lambda^3
+  fp2_mul(R, vv, T.x);
+  fp2_mul(A, u, T.z);
+  fp2_sub(A, A, vvv);
+  fp2_sub(A, A, R);
+  fp2_sub(A, A, R);
+  fp2_mul(T.x, la, A);
+  fp2_neg(T.x, T.x);       // X3 = v A
+  fp2_sub(t, R, A);
+  fp2_mul(t, th, t);
+  fp2_neg(t, t);           // u (R - A)
+  fp2_mul(R, vvv, T.y);
+  fp2_sub(T.y, t, R);
+  fp2_mul(T.z, vvv, T.z);
+}
+
 // one lane per pair (serial lines_range): a quarter of the quad's instructions per pair,
 // for launches that fill the chip on their own
 __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first, uint32_t count,
@@ -113,8 +188,27 @@ __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first,
                                                    uint32_t *L) {
   uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= count) return;
-  g2a Q = H[first + i];
-  lines_range(L, np, first + i, Q, e0, e1, Ts);
+  const uint32_t pair = first + i;
+  const g2a Q = H[pair];
+  if (aff_is_inf(Q)) {
+    lines_range(L, np, pair, Q, e0, e1, Ts);  // identity lines
+    return;
+  }
+  g2h T;
+  if (e0 > 0) {
+    T = Ts[pair];
+  } else {
+    T.x = Q.x;
+    T.y = Q.y;
+    fp2_one(T.z);
+  }
+  for (int e = e0; e < e1; e++) {
+    if (ev_is_dbl(e))
+      lane_line_dbl(T, L, np, pair, e - e0);
+    else
+      lane_line_add_aff(T, Q, L, np, pair, e - e0);
+  }
+  if (e1 < ML_EVENTS) Ts[pair] = T;
 }
 
 // one wave per pair (bls_w4.h), the smallest launches: a doubling step is six rounds of four
