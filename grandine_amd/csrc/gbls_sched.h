@@ -9,6 +9,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstddef>
@@ -126,6 +127,11 @@ struct Config {
   size_t max_merged_block = 8192;   // block import: the latency cap
   size_t merge_target = 512;        // a new leader's collection window ends at this many sets
   int merge_window_us = 300;        // ... or after this long (only while another is in flight)
+  // while *hold > 0 (a block import in progress), a normal request does not start a new
+  // submission for up to hold_max_us: the block shares the GPU only with the normal
+  // submissions already running (null: never hold)
+  const std::atomic<int> *hold = nullptr;
+  int hold_max_us = 4000;
 };
 
 // Runs the requests of `batch` (all of one kind) as ONE segmented verification: the merged
@@ -227,8 +233,15 @@ class Coalescer {
     std::unique_lock<std::mutex> lk(mu_);
     q.push_back(&r);
     cv_.notify_all();  // a leader collecting a batch (below) sees the new request at once
-    bool waited = false;
+    bool waited = false, held = false;
     while (!r.done) {
+      if (!r.prio && !held && cfg.hold && cfg.hold->load() > 0) {
+        held = true;  // a block import is being verified: leave it the GPU for a while
+        const auto deadline =
+            std::chrono::steady_clock::now() + std::chrono::microseconds(cfg.hold_max_us);
+        cv_.wait_until(lk, deadline, [&] { return r.done || cfg.hold->load() == 0; });
+        continue;
+      }
       if (leaders < max_leaders && !q.empty()) {
         // Another submission is already in flight: the GPU is busy, so a short collection
         // window costs little latency and lets the callers that return from that submission
@@ -276,6 +289,11 @@ class Coalescer {
       }
     }
     return r.ok;
+  }
+  // wake waiting callers (e.g. when the hold of Config::hold is released)
+  void wake() {
+    std::lock_guard<std::mutex> lk(mu_);
+    cv_.notify_all();
   }
 
  private:

@@ -10,6 +10,7 @@
 #include "../../grandine_amd/csrc/bls_wave12.h"
 #include "../../grandine_amd/csrc/bls_field28.h"
 #include "../../grandine_amd/csrc/bls_curve28.h"
+#include "../../grandine_amd/csrc/bls_inv.h"
 
 using namespace gbls;
 
@@ -355,6 +356,13 @@ void h_fp12_mul_ref(const uint8_t *a576, const uint8_t *b576, uint8_t *out576) {
   std::memcpy(&b, b576, 576);
   fp12_mul(c, a, b);
   std::memcpy(out576, &c, 576);
+}
+// bls_inv.h: the safegcd inversion of the final exponentiation's easy part
+void h_fp_inv_var(const uint8_t *a48, uint8_t *out48) {
+  fp a, r;
+  std::memcpy(a.l, a48, 48);
+  fp_inv_var(r, a);
+  std::memcpy(out48, r.l, 48);
 }
 int h_fp_inv_check(const uint8_t *a48, uint8_t *out48) {
   fp a, r, t;

@@ -183,6 +183,9 @@ void coalescer_stress() {
   cfg.leaders = 2;
   cfg.max_merged = 2048;
   cfg.max_merged_block = 512;
+  std::atomic<int> hold{0};  // block calls hold new normal submissions while they run
+  cfg.hold = &hold;
+  cfg.hold_max_us = 2000;
   std::atomic<long> sets{0}, calls{0}, merged_ok{0};
   std::vector<std::thread> ths;
   const int kThreads = 32, kCalls = 150;
@@ -236,7 +239,9 @@ void coalescer_stress() {
           r.sig_status = st.data();
         }
         r.prio = block ? 1 : 0;
+        if (block) hold.fetch_add(1);
         const bool ok = co.submit(r, cfg, stub_verify);
+        if (block && hold.fetch_sub(1) == 1) co.wake();
         calls++;
         sets += (long)n;
         CHECK(r.done, "returned before done");

@@ -75,6 +75,23 @@ def test_fp_inv_binary_gcd(H):
         assert int.from_bytes(out.raw, "little") == want
 
 
+def test_fp_inv_var_safegcd(H):
+    """bls_inv.h (safegcd, 30-divstep batches, variable time) against Python's modular
+    inverse: edge values, values just below p, powers of two, and random values."""
+    import random
+    rng = random.Random(21)
+    vals = [0, 1, 2, 3, O.P - 1, O.P - 2, (O.P - 1) // 2, (O.P + 1) // 2, 1 << 380, (1 << 381) % O.P]
+    vals += [(1 << k) % O.P for k in range(0, 381, 29)]
+    vals += [rng.randrange(1, O.P) for _ in range(3000)]
+    vals += [rng.randrange(1, 1 << rng.randrange(1, 381)) for _ in range(300)]
+    for a in vals:
+        out = ctypes.create_string_buffer(48)
+        H.h_fp_inv_var(a.to_bytes(48, "little"), out)
+        got = int.from_bytes(out.raw, "little")
+        want = 0 if a == 0 else pow(a * RINV % O.P, -1, O.P) * (1 << 384) % O.P
+        assert got == want, hex(a)
+
+
 def test_wave12_product_matches_tower_product(H):
     """The wave-cooperative Fp12 product (generated linear maps, 54 lanes) equals the
     tower Karatsuba product, including on extreme coefficients (0, 1, p-1)."""
