@@ -108,8 +108,10 @@ struct b0_src {
 
 HD void sha_fill_block(uint32_t (&blk)[16], const b0_src &src, uint32_t base, uint32_t nbytes,
                        uint64_t bitlen, bool last) {
+#pragma unroll
   for (int wi = 0; wi < 16; wi++) {
     uint32_t v = 0;
+#pragma unroll
     for (int bi = 0; bi < 4; bi++) {
       uint32_t idx = base + 4 * wi + bi;
       uint32_t byte;
@@ -129,9 +131,11 @@ HD void sha_fill_block(uint32_t (&blk)[16], const b0_src &src, uint32_t base, ui
   }
 }
 
-// expand_message_xmd(msg, DST, 256) -> 64 big-endian 32-bit words
-HD void expand_message_xmd_256(uint32_t (&out)[64], const uint8_t *msg, uint32_t mlen,
-                                 dst_ref dst) {
+// expand_message_xmd(msg, DST, 256): the 64 big-endian 32-bit words of the output go to
+// sink(k, w) as 4 chunks of 16 (k = 0..3: b_(2k+1) || b_(2k+2)), so that every array here
+// is indexed by constants (registers, no scratch).
+template <class Sink>
+HD void expand_message_xmd_256(const uint8_t *msg, uint32_t mlen, dst_ref dst, Sink &&sink) {
   sha_state s;
   sha256_init(s);
   uint32_t blk[16];
@@ -152,6 +156,7 @@ HD void expand_message_xmd_256(uint32_t (&out)[64], const uint8_t *msg, uint32_t
   uint32_t prev[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) prev[i] = 0;
+  uint32_t chunk[16];
   for (int bi = 1; bi <= 8; bi++) {
     // message: 32 bytes x || 1 byte i || dst || dstlen  = 33 + dst.len + 1 bytes
     uint32_t xw[8];
@@ -162,23 +167,29 @@ HD void expand_message_xmd_256(uint32_t (&out)[64], const uint8_t *msg, uint32_t
     uint64_t bl2 = (uint64_t)mlen2 * 8;
     sha256_init(s);
     for (uint32_t b = 0; b < nb2; b++) {
+#pragma unroll
       for (int wi = 0; wi < 16; wi++) {
         uint32_t v = 0;
+#pragma unroll
         for (int q = 0; q < 4; q++) {
-          uint32_t idx = 64 * b + 4 * wi + q;
+          const uint32_t idx = 64 * b + 4 * wi + q;
           uint32_t byte;
-          if (idx < 32)
-            byte = (xw[idx >> 2] >> (24 - 8 * (idx & 3))) & 0xff;
-          else if (idx == 32)
+          if (idx < 32) {
+            uint32_t x = 0;  // xw[idx >> 2] by a select chain (idx is not a constant)
+#pragma unroll
+            for (int t = 0; t < 8; t++) x = (idx >> 2) == (uint32_t)t ? xw[t] : x;
+            byte = (x >> (24 - 8 * (idx & 3))) & 0xff;
+          } else if (idx == 32) {
             byte = (uint32_t)bi;
-          else if (idx < 33 + dst.len)
+          } else if (idx < 33 + dst.len) {
             byte = dst.p[idx - 33];
-          else if (idx == 33 + dst.len)
+          } else if (idx == 33 + dst.len) {
             byte = dst.len;
-          else if (idx == mlen2)
+          } else if (idx == mlen2) {
             byte = 0x80;
-          else
+          } else {
             byte = 0;
+          }
           v = (v << 8) | byte;
         }
         blk[wi] = v;
@@ -190,11 +201,22 @@ HD void expand_message_xmd_256(uint32_t (&out)[64], const uint8_t *msg, uint32_t
       sha256_compress(s, blk);
     }
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      prev[i] = s.h[i];
-      out[8 * (bi - 1) + i] = s.h[i];
+    for (int i = 0; i < 8; i++) prev[i] = s.h[i];
+    if (bi & 1) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) chunk[i] = s.h[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) chunk[8 + i] = s.h[i];
+      sink((bi >> 1) - 1, chunk);
     }
   }
+}
+// the 64 output words in one array (host tests and tools)
+HD void expand_message_xmd_256(uint32_t (&out)[64], const uint8_t *msg, uint32_t mlen, dst_ref dst) {
+  expand_message_xmd_256(msg, mlen, dst, [&](int k, const uint32_t (&w)[16]) {
+    for (int i = 0; i < 16; i++) out[16 * k + i] = w[i];
+  });
 }
 
 // 64 big-endian bytes (16 BE words starting at w) mod p, in Montgomery form:
@@ -414,12 +436,24 @@ HD void clear_cofactor_g2(g2j &r, const g2j &p) {
 
 // hash_to_field (RFC 9380 §5.2, count = 2, m = 2, L = 64): msg -> u[0], u[1] in Fp2
 HD void hash_to_field_g2(fp2 (&u)[2], const uint8_t *msg, uint32_t mlen, dst_ref dst) {
-  uint32_t uni[64];
-  expand_message_xmd_256(uni, msg, mlen, dst);
-  fp_from_be64_words(u[0].c0, uni + 0);
-  fp_from_be64_words(u[0].c1, uni + 16);
-  fp_from_be64_words(u[1].c0, uni + 32);
-  fp_from_be64_words(u[1].c1, uni + 48);
+  fp e0, e1, e2, e3;
+  fp_zero(e0);
+  fp_zero(e1);
+  fp_zero(e2);
+  fp_zero(e3);
+  expand_message_xmd_256(msg, mlen, dst, [&](int k, const uint32_t (&w)[16]) {
+    fp v;
+    fp_from_be64_words(v, w);
+    // k is not a constant: selects keep the four elements in registers
+    fp_sel(e0, k == 0, e0, v);  // (c ? b : a)
+    fp_sel(e1, k == 1, e1, v);
+    fp_sel(e2, k == 2, e2, v);
+    fp_sel(e3, k == 3, e3, v);
+  });
+  u[0].c0 = e0;
+  u[0].c1 = e1;
+  u[1].c0 = e2;
+  u[1].c1 = e3;
 }
 // map_to_curve (SSWU + 3-isogeny) of one field element -> Jacobian point on E2
 template <class Pow>

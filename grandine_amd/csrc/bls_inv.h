@@ -1,9 +1,8 @@
-// Fast variable-time inversion in Fp for ONE value (the easy part of the final
-// exponentiation, bls_w12d.h): Bernstein-Yang "safegcd" divsteps in batches of 30 on signed
-// 30-bit limbs, the variable-time form (batches of zero-skipping and cancelling steps, the
-// operand length shrinking as the values do).  ~26 batches for a 381-bit input, each a few
-// hundred 32-bit instructions (signed 32x32 -> 64-bit mads for the matrix updates): tens of
-// microseconds on one lane, against ~0.3 ms for the one-lane binary GCD of bls_field.h.
+// Fast variable-time inversion in Fp (bls_field.h fp_inv: the lane kernels' affine
+// conversions, the final exponentiation's easy part in bls_w12d.h): Bernstein-Yang
+// "safegcd" divsteps in batches of 30 on signed 30-bit limbs, the variable-time form
+// (batches of zero-skipping and cancelling steps).  ~26 batches for a 381-bit input, each a few
+// hundred 32-bit instructions (signed 32x32 -> 64-bit mads for the matrix updates).
 // Every input on the verification path is public, so variable time is fine.
 //
 // Same contract as fp_inv: Montgomery form in (a R), Montgomery form out (a^-1 R), 0 -> 0.
@@ -111,14 +110,17 @@ HD void update_de(S30 &d, S30 &e, const Mat &t, const S30 &P, uint32_t pinv30) {
   e.v[NL - 1] = (int32_t)ce;
 }
 
-// [f, g] <- t [f, g] / 2^30 over the first len limbs (exact division)
-HD void update_fg(int len, S30 &f, S30 &g, const Mat &t) {
+// [f, g] <- t [f, g] / 2^30 (exact division).  Always over all NL limbs: with the operand
+// length shrinking as the values do, the limb arrays were indexed by a run-time length and
+// the compiler kept them in scratch memory (56 B per lane in every kernel with an inversion).
+HD void update_fg(S30 &f, S30 &g, const Mat &t) {
   const int32_t u = t.u, v = t.v, q = t.q, r = t.r;
   int64_t cf = (int64_t)u * f.v[0] + (int64_t)v * g.v[0];
   int64_t cg = (int64_t)q * f.v[0] + (int64_t)r * g.v[0];
   cf >>= 30;
   cg >>= 30;
-  for (int i = 1; i < len; i++) {
+#pragma unroll
+  for (int i = 1; i < NL; i++) {
     const int32_t fi = f.v[i], gi = g.v[i];
     cf += (int64_t)u * fi + (int64_t)v * gi;
     cg += (int64_t)q * fi + (int64_t)r * gi;
@@ -127,8 +129,8 @@ HD void update_fg(int len, S30 &f, S30 &g, const Mat &t) {
     g.v[i - 1] = (int32_t)cg & M30;
     cg >>= 30;
   }
-  f.v[len - 1] = (int32_t)cf;
-  g.v[len - 1] = (int32_t)cg;
+  f.v[NL - 1] = (int32_t)cf;
+  g.v[NL - 1] = (int32_t)cg;
 }
 
 // r in (-2p, p) -> r (or -r when sign < 0) in [0, p)
@@ -170,29 +172,18 @@ HD void inverse_words(uint32_t (&out)[12], const uint32_t (&x)[12]) {
     f.v[i] = P.v[i];
   }
   int32_t eta = -1;
-  int len = NL;
   for (int guard = 0; guard < 64; guard++) {  // ~26 batches for 381 bits; bound ~37
     Mat t;
     eta = divsteps30(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
     update_de(d, e, t, P, pinv30);
-    update_fg(len, f, g, t);
-    if (g.v[0] == 0) {
-      int32_t any = 0;
-      for (int j = 1; j < len; j++) any |= g.v[j];
-      if (any == 0) break;
-    }
-    const int32_t fn = f.v[len - 1], gn = g.v[len - 1];
-    int32_t cond = (int32_t)(len - 2) >> 31;
-    cond |= fn ^ (fn >> 31);
-    cond |= gn ^ (gn >> 31);
-    if (cond == 0) {  // both top limbs 0 or -1: drop one limb, folding its sign down
-      f.v[len - 2] |= (int32_t)((uint32_t)fn << 30);
-      g.v[len - 2] |= (int32_t)((uint32_t)gn << 30);
-      --len;
-    }
+    update_fg(f, g, t);
+    int32_t any = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) any |= g.v[j];
+    if (any == 0) break;
   }
   // f = +-1 (gcd 1): d = +-x^-1
-  normalize(d, f.v[len - 1], P);
+  normalize(d, f.v[NL - 1], P);
 #pragma unroll
   for (int k2 = 0; k2 < 12; k2++) {
     uint64_t acc = 0;

@@ -138,7 +138,7 @@ struct Ctx {
   // verified (created on first use, see Engine::block_reserve)
   hipStream_t own_g = nullptr, side1_g = nullptr, side2_g = nullptr;
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
-             ev_done = nullptr, ev_upl = nullptr, ev_in = nullptr, ev_out = nullptr, ev_tail = nullptr;
+             ev_done = nullptr, ev_upl = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool done_pending = false, upl_pending = false;
   int cls = 0;                        // 0: normal, 1: block import (every stream high priority)
   bool active = false;                // a call holds the lease and has begun
@@ -179,7 +179,6 @@ struct Ctx {
     HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_upl, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming));
     return true;
   }
   // CU-masked stream triple: mode 1 = main chain on the first `main_cus` CUs, sides on the
@@ -288,10 +287,6 @@ struct Device {
   uint32_t nsimd = 1024;  // 4 SIMDs per CU
   int ncu = 256;
   sched::CtxPool<Ctx> pool;  // per-class capped context pool (gbls_sched.h)
-  // Software pipeline of large submissions (see kPipelineMinSets): the event recorded where
-  // the latest large submission on this device entered its tail
-  std::mutex tail_mu;
-  hipEvent_t last_tail = nullptr;
   Buf reg;  // validator registry (replica), guarded by Engine::reg_mu
 };
 
@@ -313,7 +308,6 @@ struct Engine {
   int cu_split = 0;                 // latency-regime submissions on CU-masked streams (0: off)
   uint32_t cu_split_max = 1024;     // ... up to this many sets
   int leaders = 2;                  // coalescer leaders per device
-  bool pipeline = true;             // software pipeline of large submissions (kPipelineMinSets)
   // Block import under load (f3): while a GBLS_CALL_BLOCK call is in progress, normal-class
   // submissions run on streams masked off one CU in block_reserve (0: off), so the block's
   // waves never wait for SIMDs held by gossip kernels launched meanwhile.
@@ -391,7 +385,6 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
       g.cu_split_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LEADERS")) g.leaders = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("GBLS_BLOCK_RESERVE")) g.block_reserve = std::atoi(e);
-    if (const char *e = std::getenv("GBLS_PIPELINE")) g.pipeline = std::atoi(e) != 0;
     if (const char *e = std::getenv("GBLS_BLOCK_HOLD")) g.block_hold = std::atoi(e) != 0;
 #ifdef GBLS_EXPERIMENTS
     if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -574,15 +567,6 @@ void ml_tail(Ctx &c, hipStream_t st, const MlTables &mt, const uint32_t *T, uint
   launch_ml_horner(st, cur, nms, partials);
 }
 
-// Large submissions (throughput regime) are software-pipelined across submissions on a device:
-// each one's kernels start only when the previous large submission has reached its tail (the
-// Miller reduction levels, the Horner steps and the final exponentiation, which keep a few CUs
-// busy for ~4 ms of a 16-batch C2 step).  Without it, two submissions started together run in
-// lockstep and their tails coincide, leaving the chip mostly idle for that time; with it, one
-// submission's tail overlaps the next one's hash_to_G2.  Latency-regime submissions (blocks,
-// gossip) never wait on it.
-constexpr size_t kPipelineMinSets = 32768;
-
 // ----- the verification pipeline on device pointers.
 // Sets [0, n) grouped in segments by seg_off (HOST array, nseg + 1 entries); per segment
 // a Miller partial (no final exponentiation) and an error flag.  rands == nullptr
@@ -718,11 +702,6 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   const uint32_t *T = c.tab.as<uint32_t>();
   g2j *gpart = c.gpart.as<g2j>();
   int32_t *gpart_err = reinterpret_cast<int32_t *>(gpart + nchunks);
-  const bool pipelined = g.pipeline && n >= kPipelineMinSets;
-  if (pipelined) {  // start behind the previous large submission's tail (before the fork: every stream)
-    std::lock_guard<std::mutex> lk(d.tail_mu);
-    if (d.last_tail) HIPCHK(hipStreamWaitEvent(st, d.last_tail, 0));
-  }
   // ---- fork
   HIPCHK(hipEventRecord(c.ev_fork, st));
   HIPCHK(hipStreamWaitEvent(side1, c.ev_fork, 0));
@@ -810,11 +789,6 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     StageTimer t(S_ML_LEAF, st);
     launch_ml_group(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T + mt.plist_off,
                     T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>());
-  }
-  if (pipelined) {  // the next large submission may start now
-    HIPCHK(hipEventRecord(c.ev_tail, st));
-    std::lock_guard<std::mutex> lk(d.tail_mu);
-    d.last_tail = c.ev_tail;
   }
   ml_tail(c, st, mt, T, (uint32_t)nms, partials);
   if (st != caller) {

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SUBSET = ("test_fp_mul_random or test_g1_decode_fixtures or test_g2_decode_fixtures or "
           "test_hash_to_g2_fixtures or test_verify_fixtures or test_multi_verify_fixtures or "
-          "test_inversion_free_final_verdict or test_fp_inv_binary_gcd or test_fp_inv_var_safegcd or r28")
+          "test_inversion_free_final_verdict or test_fp_inv or test_fp_inv_var_safegcd or r28")
 
 
 def test_host_harness_under_asan_ubsan():

@@ -121,6 +121,128 @@ def mont(x):
     return x * R % P
 
 
+def gs_plan():
+    """Granger-Scott cyclotomic squaring on the row engine (bls_w12d.h cyc_sqr), for elements
+    of the cyclotomic subgroup (x^(p^6 + 1) = 1).  With Fp12 = Fp4[w]/(w^3 - s), s = w^3, the
+    element is g0 + g1 w + g2 w^2, gi = (z_2i..) pairs of Fp2 coefficients, and
+    x^2 = (3 g0^2 - 2 conj(g0)) + (3 s g2^2 + 2 conj(g1)) w + (3 g1^2 - 2 conj(g2)) w^2, each
+    Fp4 square (a + b s)^2 = (a^2 + xi b^2) + ((a + b)^2 - a^2 - b^2) s from three Fp2 squares
+    (x0 + x1)(x0 - x1), x0 x1.  The -2 z / +2 z terms are folded into the products as dual
+    products with constant multipliers (-2/3, -1/3, 2/3, 1/3, 1/6), so that every output is a
+    small combination of PRODUCTS (bounded, < 47 p) and never carries the input's size forward.
+    Coefficient index = h 6 + jj 2 + k (w^(2 jj + h), Fp2 component k); 12 = the zero slot.
+    Returns (rows, combine): rows[r] = (X, ybias, ypos, yneg, sbias, spos, sneg, kidx) for the 18
+    product rows (0..11 dual products, 12..17 single), combine[o] = (pos, neg) [(slot, weight)]
+    for the 12 output coefficients.  Checked against f12 squaring by tools/gen_dfp.py --check."""
+    KIDX = {"M23": 0, "M13": 1, "P23": 2, "P13": 3, "P16": 4}
+    pairs = [
+        dict(a=(0, 1), b=(8, 9), zx=(0, 1), zy=(8, 9)),
+        dict(a=(6, 7), b=(4, 5), zx=(2, 3), zy=(10, 11)),
+        dict(a=(2, 3), b=(10, 11), zx=(4, 5), z2=(6, 7)),
+    ]
+    rows = []
+    for p_, d in enumerate(pairs):
+        a0, a1 = d["a"]
+        b0, b1 = d["b"]
+        x0, x1 = d["zx"]
+        rows.append(([a0, a1], 1, [a0], [a1], 0, [x0], [], KIDX["M23"]))          # A0'
+        rows.append(([a0], 0, [a1], [], 0, [x1], [], KIDX["M13"]))                 # A1'
+        if p_ < 2:
+            y0, y1 = d["zy"]
+            rows.append(([a0, a1, b0, b1], 1, [a0, b0], [a1, b1], 1, [y0], [x0], KIDX["P23"]))  # C0'
+            rows.append(([a0, b0], 0, [a1, b1], [], 1, [y1], [x1], KIDX["P13"]))                 # C1'
+        else:
+            z20, z21 = d["z2"]
+            rows.append(([a0, a1, b0, b1], 1, [a0, b0], [a1, b1], 1, [z20, z21], [x0, x0], KIDX["P13"]))
+            rows.append(([a0, b0], 0, [a1, b1], [], 1, [z21], [z20, x1, x1], KIDX["P16"]))
+    for p_, d in enumerate(pairs):
+        b0, b1 = d["b"]
+        rows.append(([b0, b1], 1, [b0], [b1], 0, [], [], 255))   # B0
+        rows.append(([b0], 0, [b1], [], 0, [], [], 255))          # B1
+
+    def sl(p_):
+        return dict(A0=4 * p_, A1=4 * p_ + 1, C0=4 * p_ + 2, C1=4 * p_ + 3, B0=12 + 2 * p_, B1=13 + 2 * p_)
+
+    def t0(p_):
+        s_ = sl(p_)
+        return (([(s_["A0"], 3), (s_["B0"], 3)], [(s_["B1"], 6)]),
+                ([(s_["A1"], 6), (s_["B0"], 3), (s_["B1"], 6)], []))
+
+    def t1(p_):
+        s_ = sl(p_)
+        return (([(s_["C0"], 3)], [(s_["A0"], 3), (s_["B0"], 3)]),
+                ([(s_["C1"], 6)], [(s_["A1"], 6), (s_["B1"], 6)]))
+
+    def xt1(p_):
+        s_ = sl(p_)
+        return (([(s_["C0"], 3), (s_["A1"], 6), (s_["B1"], 6)], [(s_["A0"], 3), (s_["B0"], 3), (s_["C1"], 6)]),
+                ([(s_["C0"], 3), (s_["C1"], 6)], [(s_["A0"], 3), (s_["B0"], 3), (s_["A1"], 6), (s_["B1"], 6)]))
+
+    comb = [None] * 12
+    comb[0], comb[1] = t0(0)
+    comb[8], comb[9] = t1(0)
+    comb[2], comb[3] = t0(1)
+    comb[10], comb[11] = t1(1)
+    comb[4], comb[5] = t0(2)
+    comb[6], comb[7] = xt1(2)
+    return rows, comb
+
+
+def gs_check():
+    """The plan against Fp12 squaring on cyclotomic elements (plain integers mod p)."""
+    import random
+    inv3, inv6 = pow(3, -1, P), pow(6, -1, P)
+    kv = [(-2 * inv3) % P, (-inv3) % P, (2 * inv3) % P, inv3, inv6]
+    rows, comb = gs_plan()
+    xi = (1, 1)
+
+    def f2m(a, b):
+        return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+    def f12m(a, b):  # lists of 6 Fp2 coefficients of w^i, w^6 = xi
+        t = [(0, 0)] * 11
+        for i in range(6):
+            for j in range(6):
+                m = f2m(a[i], b[j])
+                t[i + j] = ((t[i + j][0] + m[0]) % P, (t[i + j][1] + m[1]) % P)
+        out = t[:6]
+        for k_ in range(6, 11):
+            m = f2m(t[k_], xi)
+            out[k_ - 6] = ((out[k_ - 6][0] + m[0]) % P, (out[k_ - 6][1] + m[1]) % P)
+        return out
+
+    def to_c(x):
+        c = [0] * 12
+        for i in range(6):
+            h, jj = i % 2, i // 2
+            c[6 * h + 2 * jj], c[6 * h + 2 * jj + 1] = x[i]
+        return c
+
+    def f12pow(a, e):
+        r_ = [(1, 0)] + [(0, 0)] * 5
+        while e:
+            if e & 1:
+                r_ = f12m(r_, a)
+            a = f12m(a, a)
+            e >>= 1
+        return r_
+
+    rng = random.Random(7)
+    f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+    g = f12pow(f, (P ** 6 - 1) * (P ** 2 + 1))  # cyclotomic
+    for _ in range(3):
+        c = to_c(g) + [0]
+        prods = []
+        for X, yb, yp, yn, sb, sp, sn, kidx in rows:
+            v = sum(c[i] for i in X) * (sum(c[i] for i in yp) - sum(c[i] for i in yn))
+            if kidx != 255:
+                v += (sum(c[i] for i in sp) - sum(c[i] for i in sn)) * kv[kidx]
+            prods.append(v % P)
+        got = [(sum(prods[i] * w_ for i, w_ in pos) - sum(prods[i] * w_ for i, w_ in neg)) % P for pos, neg in comb]
+        g = f12m(g, g)
+        assert got == to_c(g)
+
+
 # Fp2 arithmetic for the Frobenius constants: (a0, a1) = a0 + a1 u, u^2 = -1
 def f2_mul(a, b):
     return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
@@ -167,6 +289,13 @@ def main():
         # the squaring's (x0 - x1) operands subtract <= 4 coefficients (< 128 p each, limbs
         # < 2^28 + 2^9): 1024 p with 5 units borrowed per limb
         "BIAS_SQ": rebalanced(1024 * P, 5),
+        # cyclotomic squaring operands: Y subtracts <= 2 coefficients, S <= 3 (< 128 p each; 2x
+        # headroom, as BIAS_SQ, so that the unborrowed top limb never goes negative)
+        "BIAS_GY": rebalanced(512 * P, 3),
+        "BIAS_GS": rebalanced(1024 * P, 4),
+        # the easy part's inversion (bls_w12d.h inv_fp): inverse_words(x 2^384) = x^-1 2^-384,
+        # times 2^1280 / 2^448 -> x^-1 2^448
+        "INVFIX": limbs(pow(2, 1280, P)),
         # G2 endomorphisms (bls_w4.h): psi = (conj(x) cx, conj(y) cy) with cx = (0, PSI_CX1);
         # psi^2 = (x PSI2_CX, y PSI2_CY), both in Fp
         "PSI_CX1": limbs(mont(cx[1])),
@@ -222,6 +351,41 @@ def main():
     w("__constant__ uint8_t W12S_R2[12][5] = {")
     for row in sr2:
         w("  {%s}," % ", ".join(str(v) for v in row))
+    w("};")
+    gs_check()
+    grows, gcomb = gs_plan()
+    w("// Granger-Scott cyclotomic squaring (bls_w12d.h cyc_sqr; tools/gen_dfp.py gs_plan), packed per")
+    w("// row.  Product rows 0..17, word 0: X coefficients (4 nibbles), Y positive (2), Y negative (2);")
+    w("// word 1: S positive (2 nibbles), S negative (3), bit 20 Y bias, bit 21 S bias, bits 22..24 the")
+    w("// K_GS index (7: a single product).  Coefficient 12 = zero.  Combine rows 0..11: 4 positive then")
+    w("// 4 negative terms, one byte each: product slot (bits 0..6; W12D_ZERO = none), bit 7 = weight 2")
+    w("// (else 1); the output is 3 (BIAS_R1 + positive - negative).")
+    pad = lambda l, n, z: list(l) + [z] * (n - len(l))
+    w("__constant__ uint32_t W12G_ROW[18][2] = {")
+    for X, yb, yp, yn, sb, sp, sn, kidx in grows:
+        nib = pad(X, 4, 12) + pad(yp, 2, 12) + pad(yn, 2, 12)
+        w0 = sum(v << (4 * k) for k, v in enumerate(nib))
+        nib = pad(sp, 2, 12) + pad(sn, 3, 12)
+        w1 = sum(v << (4 * k) for k, v in enumerate(nib)) | yb << 20 | sb << 21 | (7 if kidx == 255 else kidx) << 22
+        w("  {0x%08xu, 0x%08xu}," % (w0, w1))
+    w("};")
+    w("__constant__ uint32_t W12G_COMB[12][2] = {")
+    zero_slot = 72
+    for pos, neg in gcomb:
+        by = []
+        for t_ in pad(pos, 4, None) + pad(neg, 4, None):
+            if t_ is None:
+                by.append(zero_slot)
+            else:
+                assert t_[1] in (3, 6)
+                by.append(t_[0] | (128 if t_[1] == 6 else 0))
+        w("  {0x%08xu, 0x%08xu}," % (sum(v << (8 * k) for k, v in enumerate(by[:4])), sum(v << (8 * k) for k, v in enumerate(by[4:]))))
+    w("};")
+    inv3, inv6 = pow(3, -1, P), pow(6, -1, P)
+    w("// the folded z terms' multipliers -2/3, -1/3, 2/3, 1/3, 1/6 (Montgomery row form)")
+    w("__constant__ uint32_t K_GS[5][16] = {")
+    for v in [(-2 * inv3) % P, (-inv3) % P, (2 * inv3) % P, inv3, inv6]:
+        w("  {%s}," % ", ".join("0x%08xu" % x for x in limbs(mont(v))))
     w("};")
     w("// Frobenius constants by exponent e of w: FROB1[e] = (c0, c1) of xi^(e (p - 1) / 6),")
     w("// FROB2[e] = xi^(e (p^2 - 1) / 6) (in Fp); e = 0 is one")
