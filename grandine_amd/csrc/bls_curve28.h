@@ -78,7 +78,8 @@ HD void g2_psi2_28(g2j28 &r, const g2j28 &p) {
   r.z = p.z;
 }
 
-// h_eff P, the sequence of clear_cofactor_g2 (bls_hash.h, Budroni-Pintore)
+// h_eff P, the sequence of clear_cofactor_g2 (bls_hash.h, Budroni-Pintore): host tests of
+// the layer's G2 formulas (tests/native/host_harness.cpp)
 HD void clear_cofactor28(g2j28 &r, const g2j28 &p) {
   g2j28 t1, t2, t3;
   mul_by_xabs(t1, p);
@@ -97,51 +98,6 @@ HD void clear_cofactor28(g2j28 &r, const g2j28 &p) {
   jac_add(t3, t3, t1);  // - psi(P)
   jac_neg(t1, p);
   jac_add(r, t3, t1);  // - P
-}
-
-// [|x|]B with the base B parked (bls_curve.h mul_by_xabs): the 63 doublings keep only the
-// accumulator in registers, the 5 additions reload B
-template <class Park>
-HD void mul_by_xabs_parked(g2j28 &r, const Park &base) {
-  base.get(r);
-  for (int i = 62; i >= 0; i--) {
-    jac_dbl(r, r);
-    if ((k::X_ABS >> i) & 1) {
-      g2j28 b;
-      base.get(b);
-      jac_add(r, r, b);
-    }
-  }
-}
-// The same h_eff P in the RFC 9380 G.3 order with two parked points (`pb`: the chain base,
-// `pt`: the running T), so that the [x] chains hold one point plus the formula temporaries:
-//   t1 = [x]P;  t2 = t1 + psi(P);  T = psi^2(2P) - psi(P) - P - t1;  h = T + [x] t2.
-template <class ParkB, class ParkT>
-HD void clear_cofactor28_parked(g2j28 &r, const g2j28 &p, const ParkB &pb, const ParkT &pt) {
-  g2j28 t1, t2;
-  g2_psi28(t2, p);       // psi(P)
-  jac_dbl(t1, p);
-  g2_psi2_28(t1, t1);    // psi^2(2P)
-  jac_neg(t2, t2);
-  jac_add(t1, t1, t2);   // psi^2(2P) - psi(P)
-  jac_neg(t2, p);
-  jac_add(t1, t1, t2);   // ... - P
-  pt.put(t1);
-  pb.put(p);
-  mul_by_xabs_parked(t1, pb);
-  jac_neg(t1, t1);       // t1 = [x]P
-  pb.get(t2);
-  g2_psi28(t2, t2);
-  jac_add(t2, t2, t1);   // t2 = t1 + psi(P)
-  pb.put(t2);
-  jac_neg(t1, t1);
-  pt.get(t2);
-  jac_add(t2, t2, t1);   // T = psi^2(2P) - psi(P) - P - t1
-  pt.put(t2);
-  mul_by_xabs_parked(t1, pb);
-  jac_neg(t1, t1);       // [x] t2
-  pt.get(t2);
-  jac_add(r, t2, t1);
 }
 
 }  // namespace r28

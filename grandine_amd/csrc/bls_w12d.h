@@ -36,6 +36,13 @@ struct Eng {
   const uint32_t *pl;  // this row's plan words (ws + PLAN + PW row)
 };
 
+// The cyclotomic squaring's product row on physical row r, or -1.  Waves go to the 4 SIMDs
+// round-robin (wave w on SIMD w mod 4): GS rows 0..11 (dual products) fill waves 0..2, the
+// single products 12..15 wave 3 and 16..17 wave 7, so SIMD 0..2 each run one wave of dual
+// products and SIMD 3 two waves of single ones (rows 16..17 on wave 4 put a dual and a single
+// wave on SIMD 0: 2.6 single-product times against 2 here).
+__device__ __forceinline__ int gs_row(uint32_t r) { return r < 16 ? (int)r : (r == 28 || r == 29) ? (int)r - 12 : -1; }
+
 __device__ __forceinline__ uint32_t byte_of(const uint32_t *w, int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xffu; }
 
 // every thread of the workgroup; ws = WS words of LDS
@@ -81,8 +88,9 @@ __device__ __forceinline__ void begin(Eng &e, uint32_t *ws) {
   w[P_S2 + 0] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
   w[P_S2 + 1] = b[4];
   // cyclotomic squaring plan (18 product rows, 12 combine rows)
-  w[P_G + 0] = r < 18 ? dfp::W12G_ROW[r][0] : 0xccccccccu;
-  w[P_G + 1] = r < 18 ? dfp::W12G_ROW[r][1] : 0x01cccccu;
+  const int gr = gs_row(r);
+  w[P_G + 0] = gr >= 0 ? dfp::W12G_ROW[gr][0] : 0xccccccccu;
+  w[P_G + 1] = gr >= 0 ? dfp::W12G_ROW[gr][1] : 0x01cccccu;
   w[P_GC + 0] = r < 12 ? dfp::W12G_COMB[r][0] : 0x48484848u;
   w[P_GC + 1] = r < 12 ? dfp::W12G_COMB[r][1] : 0x48484848u;
   if (e.j == 0) {
@@ -191,7 +199,8 @@ __device__ __forceinline__ void sqr(Eng &e, uint32_t *c, const uint32_t *a) {
 // 512 p + <= 2 - <= 2 coefficients (< 768 p), S = 1024 p + <= 2 - <= 3 coefficients
 // (< 1280 p < 2^392); outputs 3 (8 p + <= 5 - <= 6 products) < 40 p.  All threads call it.
 __device__ __forceinline__ void cyc_sqr(Eng &e, uint32_t *c, const uint32_t *a) {
-  if (e.row < 18) {
+  const int gr = gs_row(e.row);
+  if (gr >= 0) {
     const uint32_t *zero = e.ws + 16 * dfp::W12D_ZERO;
     const uint32_t w0 = e.pl[P_G], w1 = e.pl[P_G + 1], j = e.j;
     auto co = [&](uint32_t q) { return (q == 12 ? zero : a + 16 * q)[j]; };
@@ -208,7 +217,7 @@ __device__ __forceinline__ void cyc_sqr(Eng &e, uint32_t *c, const uint32_t *a) 
       z -= co((w1 >> 8) & 15u) + co((w1 >> 12) & 15u) + co((w1 >> 16) & 15u);
       p = dfp::mul2(dfp::norm(x), dfp::norm(y), dfp::norm(z), e.ws[GSK + 16 * ((w1 >> 22) & 7u) + j], e.t);
     }
-    e.ws[16 * e.row + j] = p;
+    e.ws[16 * gr + j] = p;
   }
   __syncthreads();
   if (e.row < 12) {

@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n,
 // kernel spilled 100 B per lane; here each chain holds only its base, its accumulator and the
 // addition's temporaries, and the points between the chains wait in the message's own two Q
 // slots in HBM (576 B per message).  The same group element as clear_cofactor_g2 (RFC 9380
-// G.3 order, as clear_cofactor28_parked):
+// G.3 order):
 //   a: P = Q0 + Q1;  t1 = [x]P;  t2 = t1 + psi(P) -> Q[2i];  T = psi^2(2P) - psi(P) - P - t1 -> Q[2i+1]
 //   b: h = [x] t2 + T -> affine H[i]
 __global__ void __launch_bounds__(WG) k_h2c_clear_lane_a(g2j *Q, uint32_t n) {
@@ -188,50 +188,8 @@ bool launch_h2c_clear_jac(hipStream_t st, g2j *Q, uint32_t n) {
   return true;
 }
 
-// the lane form in the radix-2^28 layer (bls_curve28.h): Q0 + Q1 in the engine form, the
-// 126 doublings and 10 additions of h_eff with 14-limb products (one v_mad_u64_u32 per term, no
-// carry word), back to the engine form for the affine conversion
-// a lane's parked point, word k at slot[k * stride] (LDS: stride WG, conflict-free; global:
-// the lane's own Q[2i], Q[2i + 1] words, free once read)
-struct Park28 {
-  uint32_t *slot;
-  uint32_t stride;
-  __device__ void put(const r28::g2j28 &v) const {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(&v);
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(r28::g2j28) / 4); k++) slot[k * stride] = w[k];
-  }
-  __device__ void get(r28::g2j28 &v) const {
-    uint32_t *w = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(r28::g2j28) / 4); k++) w[k] = slot[k * stride];
-  }
-};
-static_assert(sizeof(r28::g2j28) <= 2 * sizeof(g2j), "T parks in the lane's two Q slots");
-__global__ void __launch_bounds__(WG) k_h2c_clear_lane28(g2j *Q, uint32_t n, g2a *H) {
-  __shared__ uint32_t park[(sizeof(r28::g2j28) / 4) * WG];
-  uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  g2j a = Q[2 * i], b = Q[2 * i + 1];
-  jac_add(a, a, b);
-  r28::g2j28 p, h;
-  r28::g2j_in(p, a);
-  r28::clear_cofactor28_parked(h, p, Park28{park + threadIdx.x, WG},
-                               Park28{reinterpret_cast<uint32_t *>(Q + 2 * i), 1});
-  r28::g2j_out(a, h);
-  g2a o;
-  jac_to_aff(o, a);
-  H[i] = o;
-}
-
 void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   if (!n) return;
-#if defined(GBLS_CLEAR_R28)  // measured A/B on MI355X: C2 3.847M vs 3.856M sets/s (520 B spills)
-  if (n >= kLaneRegimeClear) {
-    k_h2c_clear_lane28<<<nblk(n), WG, 0, st>>>(const_cast<g2j *>(Q), n, H);  // Q is a scratch of the call
-    return;
-  }
-#endif
   if (n <= kW4Max)
     (n <= w4::kExclusiveMaxWaves ? k_h2c_clear_w4<true> : k_h2c_clear_w4<false>)<<<n, 64, 0, st>>>(Q, n, H);
   else if (n >= kLaneRegimeClear) {
