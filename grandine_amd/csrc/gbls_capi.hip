@@ -308,6 +308,8 @@ struct Engine {
   int cu_split = 0;                 // latency-regime submissions on CU-masked streams (0: off)
   uint32_t cu_split_max = 1024;     // ... up to this many sets
   int leaders = 2;                  // coalescer leaders per device
+  size_t merge_target = 768;        // a new gossip leader's collection target (gbls_sched.h)
+  int merge_window_us = 300;        // ... and its longest wait
   // Block import under load (f3): while a GBLS_CALL_BLOCK call is in progress, normal-class
   // submissions run on streams masked off one CU in block_reserve (0: off), so the block's
   // waves never wait for SIMDs held by gossip kernels launched meanwhile.
@@ -384,6 +386,8 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_CU_SPLIT_MAX"))
       g.cu_split_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LEADERS")) g.leaders = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("GBLS_MERGE_TARGET")) g.merge_target = std::strtoull(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_MERGE_WINDOW_US")) g.merge_window_us = std::atoi(e);
     if (const char *e = std::getenv("GBLS_BLOCK_RESERVE")) g.block_reserve = std::atoi(e);
     if (const char *e = std::getenv("GBLS_BLOCK_HOLD")) g.block_hold = std::atoi(e) != 0;
 #ifdef GBLS_EXPERIMENTS
@@ -1111,6 +1115,8 @@ bool coalesced_verify(CoReq &r) {
   cfg.coalesce = g.coalesce.load();
   cfg.devices = (int)g.devs.size();
   cfg.leaders = g.leaders;
+  cfg.merge_target = g.merge_target;
+  cfg.merge_window_us = g.merge_window_us;
   if (g.block_hold) cfg.hold = &g.block_active;
   bool ok = co.submit(r, cfg, [](CoReq &m) {
     m.ok = verify_host(m.msgs, m.sigs, m.sigs_c, m.sig_status, m.src, m.rands, m.n, m.seg_off,

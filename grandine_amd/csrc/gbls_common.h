@@ -100,7 +100,10 @@ struct MsmPlan {
   uint32_t extra;       // extra Miller pairs per segment: W (tree) or W * 2^(c-1)
   size_t o_cnt, o_start, o_cur, o_cstart, o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
 };
-constexpr uint32_t kMsmMinPerSeg = 2048;  // default: segments at least this large use the MSM
+// default: segments at least this large use the bucket MSM (2048 -> 4096 in r04: a C4 epoch of
+// 2048-set segments ran 542-572k sets/s with per-set products vs 375-390k with the MSM,
+// profiles/r04/k_*; C2 and C5 segments are >= 4096)
+constexpr uint32_t kMsmMinPerSeg = 4096;
 MsmPlan msm_plan(uint32_t n, uint32_t nseg);
 // writes each segment's p.extra Miller pairs (P[n + s * extra + k] = a constant G1 weight,
 // H[...] = affine bucket or window sum), zeroes seg_err and flags empty segments when

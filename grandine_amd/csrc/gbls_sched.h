@@ -125,7 +125,7 @@ struct Config {
   int leaders = 2;                  // normal leaders per device (block import: 1 per device)
   size_t max_merged = 1 << 16;      // merged normal submissions stay below one C2 step
   size_t max_merged_block = 8192;   // block import: the latency cap
-  size_t merge_target = 512;        // a new leader's collection window ends at this many sets
+  size_t merge_target = 768;        // a new leader's collection window ends at this many sets
   int merge_window_us = 300;        // ... or after this long (only while another is in flight)
   // while *hold > 0 (a block import in progress), a normal request does not start a new
   // submission for up to hold_max_us: the block shares the GPU only with the normal

@@ -12,6 +12,8 @@ from grandine_amd import factory as F  # noqa: E402
 
 secs = float(sys.argv[1]) if len(sys.argv) > 1 else 3.0
 nthr = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+if "--tuning" in sys.argv:  # GBLS_MERGE_TARGET / GBLS_LEADERS / ... sweeps
+    G.enable_tuning()
 L = G.lib()
 gm, gs, gp, gr = F.c2_batch(64, seed=64)
 r64 = (ctypes.c_uint64 * 64)(*gr)
