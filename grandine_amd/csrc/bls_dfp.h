@@ -107,7 +107,11 @@ __device__ __forceinline__ void pass_lo32(uint64_t &lo, uint64_t &hi, uint32_t j
 }
 
 // T += a b: lane j accumulates column j (lo) and column j + 16 (hi).  a, b have 14 limbs.
+// Odd and even terms go to separate accumulators (GBLS_DFP_ONE_ACC: one chain), so the 64-bit
+// multiply-adds form two independent dependency chains: a lone wave (the latency regime's
+// chains) otherwise waits on every accumulate.
 __device__ __forceinline__ void columns(uint64_t &lo, uint64_t &hi, uint32_t a, uint32_t b) {
+#if defined(GBLS_DFP_ONE_ACC)
   lo += (uint64_t)bcast<0>(a) * b;
   For<1, 14>::run([&](auto I) {
     constexpr int i = decltype(I)::value;
@@ -115,6 +119,23 @@ __device__ __forceinline__ void columns(uint64_t &lo, uint64_t &hi, uint32_t a, 
     lo += (uint64_t)ai * shr<i>(b);       // b_(j-i), j >= i
     hi += (uint64_t)ai * shl<16 - i>(b);  // b_(j+16-i), j < i
   });
+#else
+  uint64_t lo1 = 0, hi1 = 0;
+  lo += (uint64_t)bcast<0>(a) * b;
+  For<1, 14>::run([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const uint32_t ai = bcast<i>(a);
+    if constexpr (i & 1) {
+      lo1 += (uint64_t)ai * shr<i>(b);       // b_(j-i), j >= i
+      hi1 += (uint64_t)ai * shl<16 - i>(b);  // b_(j+16-i), j < i
+    } else {
+      lo += (uint64_t)ai * shr<i>(b);
+      hi += (uint64_t)ai * shl<16 - i>(b);
+    }
+  });
+  lo += lo1;
+  hi += hi1;
+#endif
 }
 __device__ __forceinline__ uint32_t redc(uint64_t lo, uint64_t hi, const Tabs &t);
 
@@ -141,6 +162,7 @@ __device__ __forceinline__ uint32_t redc(uint64_t lo, uint64_t hi, const Tabs &t
   pass_lo32(lo, hi, j);
   const uint32_t tl = (uint32_t)lo;
   // m = T_lo p' mod 2^448: column j = sum over i <= j of p'_i t_(j-i)
+#if defined(GBLS_DFP_ONE_ACC)
   uint64_t mc = (uint64_t)K_PINV_U[0] * tl;
   For<1, 16>::run([&](auto I) {
     constexpr int i = decltype(I)::value;
@@ -154,6 +176,32 @@ __device__ __forceinline__ uint32_t redc(uint64_t lo, uint64_t hi, const Tabs &t
     lo += (uint64_t)K_P_U[i] * shr<i>(m);       // m_(j-i), j >= i
     hi += (uint64_t)K_P_U[i] * shl<16 - i>(m);  // m_(j+16-i), j < i
   });
+#else
+  uint64_t mc = (uint64_t)K_PINV_U[0] * tl, mc1 = 0;
+  For<1, 16>::run([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (i & 1)
+      mc1 += (uint64_t)K_PINV_U[i] * shr<i>(tl);
+    else
+      mc += (uint64_t)K_PINV_U[i] * shr<i>(tl);
+  });
+  const uint32_t m = norm64(mc + mc1);
+  // U = T + m p (p_i uniform, m shifted across the row); U_lo = 0 mod 2^448
+  uint64_t lo1 = 0, hi1 = 0;
+  lo += (uint64_t)K_P_U[0] * m;
+  For<1, 14>::run([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (i & 1) {
+      lo1 += (uint64_t)K_P_U[i] * shr<i>(m);       // m_(j-i), j >= i
+      hi1 += (uint64_t)K_P_U[i] * shl<16 - i>(m);  // m_(j+16-i), j < i
+    } else {
+      lo += (uint64_t)K_P_U[i] * shr<i>(m);
+      hi += (uint64_t)K_P_U[i] * shl<16 - i>(m);
+    }
+  });
+  lo += lo1;
+  hi += hi1;
+#endif
   // carry of U_lo into column 16: after two passes the low limbs are < 2^28 + 2^9 and their
   // value, a multiple of 2^448 below 2^449, is 2^448 exactly when any limb is nonzero
   pass_lo64(lo, hi, j);

@@ -145,7 +145,7 @@ struct Ctx {
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
-  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, Sj, gpart, lines, Ts, V0, V1, tab, part, err, out0,
+  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, Sj, gpart, lines, Ts, V0, V1, hparts, tab, part, err, out0,
       out1, pks, pre, pre2, msm, sigd, sigst, rnd, ng1, gerr, gv, redo, rtab;
   // per-call option of the next pipeline_partials on this lease: compressed signatures
   // (96 B each, device) to decompress on the signature-side stream into `sigs`, with their
@@ -557,8 +557,12 @@ MlTables ml_tables(std::vector<uint32_t> &tab, size_t nms, size_t npairs, int EC
 }
 
 // the reduction levels and the Horner step after k_ml_group (products in c.V0)
+// submissions up to this many sets split their Horner chains (latency regime: blocks, gossip
+// merges, single C2 batches, a C4 epoch); larger ones (many batches) keep one chain
+constexpr size_t kSplitHornerMaxSets = 8192;
+
 void ml_tail(Ctx &c, hipStream_t st, const MlTables &mt, const uint32_t *T, uint32_t nms,
-             fp12 *partials) {
+             fp12 *partials, bool split) {
   fp12 *cur = c.V0.as<fp12>(), *other = c.V1.as<fp12>();
   {
     StageTimer t(S_ML_REDUCE, st);
@@ -568,7 +572,11 @@ void ml_tail(Ctx &c, hipStream_t st, const MlTables &mt, const uint32_t *T, uint
     }
   }
   StageTimer t(S_ML_HORNER, st);
-  launch_ml_horner(st, cur, nms, partials);
+  // latency regime: the Horner chain split in 4 parts (their values in a buffer of their own,
+  // ensured with the workspaces); throughput regime: one chain (the parts' extra squarings
+  // only cost there, where another submission fills the chip during the tail)
+  fp12 *tmp = split && nms <= 64 ? c.hparts.as<fp12>() : nullptr;
+  launch_ml_horner(st, cur, nms, partials, nullptr, 0, tmp);
 }
 
 // ----- the verification pipeline on device pointers.
@@ -692,7 +700,8 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
       !c.ensure(c.R, 2 * n * sizeof(g2j) + 16) ||
       !c.ensure(c.gpart, nchunks * (sizeof(g2j) + 4)) || !c.ensure(c.lines, line_words * 4) ||
       !c.ensure(c.V0, ML_EVENTS * mt.v0_n * sizeof(fp12)) ||
-      !c.ensure(c.V1, ML_EVENTS * mt.v1_n * sizeof(fp12)))
+      !c.ensure(c.V1, ML_EVENTS * mt.v1_n * sizeof(fp12)) ||
+      !c.ensure(c.hparts, 4 * 64 * sizeof(fp12)))  // the split Horner's parts (<= 64 segments)
     return false;
   if (!c.upload_staged(c.tab, tab.data(), tab.size() * 4, st)) return false;
   const uint32_t N = (uint32_t)n, NP = (uint32_t)np, NS = (uint32_t)nseg;
@@ -794,7 +803,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     launch_ml_group(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T + mt.plist_off,
                     T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>());
   }
-  ml_tail(c, st, mt, T, (uint32_t)nms, partials);
+  ml_tail(c, st, mt, T, (uint32_t)nms, partials, n <= kSplitHornerMaxSets);
   if (st != caller) {
     HIPCHK(hipEventRecord(c.ev_out, st));
     HIPCHK(hipStreamWaitEvent(caller, c.ev_out, 0));
@@ -1806,13 +1815,14 @@ int gbls_hash_to_g2(const uint8_t *msg_data, const uint32_t *msg_off, size_t n, 
                     size_t dst_len, gbls_p2_affine *out) {
   API_BEGIN
   if (n == 0) return GBLS_SUCCESS;
-  if (dst_len > 255) return fail(GBLS_ERR_ARG), FAILED;
+  // dst == NULL (with dst_len 0): the signature scheme's own DST (BLS_SIG_..._POP_)
+  if (dst_len > 255 || !msg_data || !msg_off || !out || (!dst && dst_len)) return fail(GBLS_ERR_ARG), FAILED;
   Lease L(pick_device());
   Ctx &c = *L;
   hipStream_t st = c.own;
-  if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in3, dst, dst_len ? dst_len : 1, st))
+  if (!L.ok() || !c.begin(st) || (dst && !c.upload_staged(c.in3, dst, dst_len ? dst_len : 1, st)))
     return FAILED;
-  if (!h2c_affine(c, msg_data, msg_off, n, c.in3.as<uint8_t>(), (uint32_t)dst_len, st))
+  if (!h2c_affine(c, msg_data, msg_off, n, dst ? c.in3.as<uint8_t>() : nullptr, (uint32_t)dst_len, st))
     return FAILED;
   if (hipMemcpyAsync(out, c.out1.p, n * sizeof(g2a), hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)

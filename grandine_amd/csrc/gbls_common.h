@@ -133,8 +133,9 @@ void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);
 // lim (device count, optional): only segments s with base + s < *lim run (the others exit)
+// tmp (optional, >= 4 nseg values): up to 64 segments run the chain in 4 parallel parts
 void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial,
-                      const uint32_t *lim = nullptr, uint32_t base = 0);
+                      const uint32_t *lim = nullptr, uint32_t base = 0, fp12 *tmp = nullptr);
 
 // k_fexp.hip -- product of partials, final exponentiation, verdict
 // lim / base as in launch_ml_horner; scatter (optional): segment s's verdict goes to

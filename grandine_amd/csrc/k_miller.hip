@@ -157,31 +157,60 @@ void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint3
   if (nout) k_ml_reduce<<<grid, 64, 0, st>>>(Vin, nin, red, nout, Vout);
 }
 // k_ml_horner on the row-distributed Fp12 engine (bls_w12d.h), for launches of a few
-// segments: all 68 event values of the segment are staged in LDS first (52 KB), then the
-// 131-step chain runs one row-product per Fp12 product.  Event values are read as repacked
-// limbs (an Fp* scalar each; the final exponentiation removes them); the partial is written
-// as canonical engine-form words.
+// segments, with the 68-event chain SPLIT into parts that run side by side (one workgroup
+// each, grid (nseg, parts)): f = prod_k V_k^(2^(D_k)) (D_k = doubling events after k), so part
+// [a, b) computes its own Horner value and then squares it once per doubling event after b;
+// the parts' products are f.  With 4 parts the longest chain is 53.5 product-times instead of
+// 113.5 (squarings at 0.75; tools/gpu notes in DESIGN.md section 9), and k_ml_combine_d
+// multiplies the 4 values.  Event values are read as repacked limbs (an Fp* scalar each; the
+// final exponentiation removes them); every part is conj'd (conj is a field automorphism).
+struct HornerParts {
+  int n;
+  int b[8];  // part p covers events [b[p], b[p + 1])
+};
+constexpr HornerParts kHornerParts4 = {4, {0, 7, 18, 36, 68, 68, 68, 68}};
+constexpr HornerParts kHornerParts1 = {1, {0, 68, 68, 68, 68, 68, 68, 68}};
+
 __global__ void __launch_bounds__(w12d::THREADS) k_ml_horner_d(const fp12 *V, uint32_t nseg,
-                                                               fp12 *partial, const uint32_t *lim,
-                                                               uint32_t base) {
+                                                               fp12 *out, const uint32_t *lim,
+                                                               uint32_t base, HornerParts hp) {
   __shared__ __attribute__((aligned(16))) uint32_t ev[ML_EVENTS * w12d::IMG], acc[w12d::IMG],
       ws[w12d::WS];
-  const uint32_t s = blockIdx.x;
+  const uint32_t s = blockIdx.x, part = blockIdx.y;
   if (lim && base + s >= *lim) return;  // block-uniform
+  const int e0 = hp.b[part], e1 = hp.b[part + 1];
   w12d::Eng e;
   w12d::begin(e, ws);
-  for (uint32_t q = e.row; q < (uint32_t)ML_EVENTS * 12; q += w12d::ROWS) {
+  for (uint32_t q = e.row; q < (uint32_t)(e1 - e0) * 12; q += w12d::ROWS) {
     const uint32_t ev_i = q / 12, c = q % 12;
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(V + (size_t)ev_i * nseg + s) + 12 * c;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(V + (size_t)(e0 + ev_i) * nseg + s) + 12 * c;
     ev[ev_i * w12d::IMG + 16 * c + e.j] = dfp::from_words_scaled(w);
   }
   __syncthreads();
   w12d::copy(e, acc, ev);
-  for (int k = 1; k < ML_EVENTS; k++) {
+  for (int k = e0 + 1; k < e1; k++) {
     if (ev_is_dbl(k)) w12d::sqr(e, acc, acc);
-    w12d::mul(e, acc, acc, ev + k * w12d::IMG);
+    w12d::mul(e, acc, acc, ev + (k - e0) * w12d::IMG);
   }
+  for (int k = e1; k < ML_EVENTS; k++)
+    if (ev_is_dbl(k)) w12d::sqr(e, acc, acc);
   w12d::conj(e, acc, acc);
+  w12d::store_words(e, reinterpret_cast<uint32_t *>(out + (size_t)part * nseg + s), acc);
+}
+// partial[s] = prod_p parts[p][s] (row engine; canonical words out)
+__global__ void __launch_bounds__(w12d::THREADS) k_ml_combine_d(const fp12 *parts, uint32_t nparts,
+                                                                uint32_t nseg, fp12 *partial,
+                                                                const uint32_t *lim, uint32_t base) {
+  __shared__ __attribute__((aligned(16))) uint32_t acc[w12d::IMG], tmp[w12d::IMG], ws[w12d::WS];
+  const uint32_t s = blockIdx.x;
+  if (lim && base + s >= *lim) return;  // block-uniform
+  w12d::Eng e;
+  w12d::begin(e, ws);
+  w12d::load_scaled(e, acc, reinterpret_cast<const uint32_t *>(parts + s));
+  for (uint32_t p = 1; p < nparts; p++) {
+    w12d::load_scaled(e, tmp, reinterpret_cast<const uint32_t *>(parts + (size_t)p * nseg + s));
+    w12d::mul(e, acc, acc, tmp);
+  }
   w12d::store_words(e, reinterpret_cast<uint32_t *>(partial + s), acc);
 }
 
@@ -189,12 +218,16 @@ __global__ void __launch_bounds__(w12d::THREADS) k_ml_horner_d(const fp12 *V, ui
 constexpr uint32_t kHornerRowsMaxSegs = 64;
 
 void launch_ml_horner(hipStream_t st, const fp12 *V, uint32_t nseg, fp12 *partial,
-                      const uint32_t *lim, uint32_t base) {
+                      const uint32_t *lim, uint32_t base, fp12 *tmp) {
   if (!nseg) return;
-  if (nseg <= kHornerRowsMaxSegs)
-    k_ml_horner_d<<<nseg, w12d::THREADS, 0, st>>>(V, nseg, partial, lim, base);
-  else
+  if (nseg <= kHornerRowsMaxSegs && tmp) {
+    k_ml_horner_d<<<dim3(nseg, kHornerParts4.n), w12d::THREADS, 0, st>>>(V, nseg, tmp, lim, base, kHornerParts4);
+    k_ml_combine_d<<<nseg, w12d::THREADS, 0, st>>>(tmp, kHornerParts4.n, nseg, partial, lim, base);
+  } else if (nseg <= kHornerRowsMaxSegs) {
+    k_ml_horner_d<<<dim3(nseg, 1), w12d::THREADS, 0, st>>>(V, nseg, partial, lim, base, kHornerParts1);
+  } else {
     k_ml_horner<<<nseg, 64, 0, st>>>(V, nseg, partial, lim, base);
+  }
 }
 
 }  // namespace gbls

@@ -270,7 +270,8 @@ int gbls_final_verify_partials_device(const gbls_fp12 *partials, const int32_t *
 int gbls_sk_to_pk(const uint8_t (*sks)[32], size_t n, gbls_p1_affine *out);
 int gbls_sign(const uint8_t (*sks)[32], const uint8_t *msg_data, const uint32_t *msg_off, size_t n,
               gbls_p2_affine *out);
-/* hash_to_G2 with an explicit DST (RFC 9380 test vectors) -> affine points */
+/* hash_to_G2 with an explicit DST (RFC 9380 test vectors) -> affine points; dst == NULL with
+ * dst_len == 0 selects the proof-of-possession scheme's DST that every verify entry uses */
 int gbls_hash_to_g2(const uint8_t *msg_data, const uint32_t *msg_off, size_t n, const uint8_t *dst,
                     size_t dst_len, gbls_p2_affine *out);
 

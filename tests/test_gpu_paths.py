@@ -186,6 +186,23 @@ def test_bad_segment_offsets_are_argument_errors(G, L, F):
         assert (v[0], v[1]) == (G.VERIFY_FAIL, G.VERIFY_FAIL)
 
 
+def test_hash_to_g2_default_dst_and_argument_errors(G, L):
+    """gbls_hash_to_g2 with dst == NULL uses the POP scheme's DST (the same points as passing it
+    explicitly); NULL with a nonzero length, or a NULL message array, is an argument error
+    (it crashed in upload before r04)."""
+    dst = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
+    n = 3
+    msgs = bytes(range(32 * n))
+    off = G.u32_array(range(0, 32 * n + 1, 32))
+    a = (ctypes.c_uint8 * (192 * n))()
+    b = (ctypes.c_uint8 * (192 * n))()
+    G.check(L.gbls_hash_to_g2(G.buf(msgs), off, n, dst, len(dst), a), "explicit dst")
+    G.check(L.gbls_hash_to_g2(G.buf(msgs), off, n, None, 0, b), "default dst")
+    assert bytes(a) == bytes(b)
+    assert L.gbls_hash_to_g2(G.buf(msgs), off, n, None, 5, b) == G.VERIFY_FAIL and L.gbls_last_error() == 102
+    assert L.gbls_hash_to_g2(None, off, n, dst, len(dst), b) == G.VERIFY_FAIL and L.gbls_last_error() == 102
+
+
 def test_concurrent_callers_threads_and_streams(G, L, F, torch_dev):
     """many threads call in at once.  8 host threads x 6 calls (host-pointer
     and device-pointer on per-thread streams), a mix of valid and corrupted batches; every
@@ -212,6 +229,9 @@ def test_concurrent_callers_threads_and_streams(G, L, F, torch_dev):
                 expect_ok = (it + t) % 2 == 0
                 if it % 3 == 2:
                     v = torch.full((1,), -1, dtype=torch.int32, device=dev)
+                    # the fill ran on this thread's current stream: order it before the call's
+                    # stream (an unordered fill can land after the verdict and read as -1)
+                    stream.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(stream):
                         rc = L.gbls_multi_verify_segments_device((dm if expect_ok else db).data_ptr(), ds.data_ptr(),
                                                                  dp.data_ptr(), dr.data_ptr(), n, seg, 1, v.data_ptr(),
