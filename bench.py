@@ -93,10 +93,10 @@ def cpu_threads():
 
 def pmc_traffic(kernel, default_cmd):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
-    summary of the default command without the one-batch leg (profiles/r04/b_c2_pmc_bytes.csv,
+    summary of the default command without the one-batch leg (profiles/r04/z_c2_pmc_bytes.csv,
     tools/prof/pmc_bytes.py, from `bench.py --no-single`: 16-batch launches only;
     FETCH_SIZE doubled per the gfx950 correction).  None for other commands or if absent."""
-    path = os.path.join(ROOT, "profiles", "r04", "b_c2_pmc_bytes.csv")
+    path = os.path.join(ROOT, "profiles", "r04", "z_c2_pmc_bytes.csv")
     if not default_cmd or not os.path.exists(path):
         return None
     with open(path) as f:

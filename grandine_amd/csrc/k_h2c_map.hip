@@ -42,7 +42,10 @@ __global__ void __launch_bounds__(WG) k_h2c_map_row(const fp2 *U, uint32_t nu, g
 }
 
 // field elements up to this many take the row form (16 lanes each: 512 waves at the limit)
-constexpr uint32_t kMapRowsMax = 2048;
+#ifndef GBLS_MAP_ROWS_MAX
+#define GBLS_MAP_ROWS_MAX 2048
+#endif
+constexpr uint32_t kMapRowsMax = GBLS_MAP_ROWS_MAX;
 
 void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q) {
   if (!nu) return;
