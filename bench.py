@@ -288,6 +288,10 @@ def main():
         d_parts = [torch.zeros(world * nb * 576, dtype=torch.uint8, device=dev) for _ in range(slots)]
         d_errs = [torch.zeros(world * nb, dtype=torch.int32, device=dev) for _ in range(slots)]
         seg = G.u32_array([n * b // nb for b in range(nb + 1)])
+        # the fills above ran on the default stream; the steps run on their own streams, which
+        # do not wait for it: without this a late fill can overwrite a warm-up step's partial
+        # or verdict (seen as "verdicts of the warm-up step are WRONG" in 2-rank runs on one GPU)
+        torch.cuda.synchronize()
         leg.units = n
         leg.segments = nb
 
@@ -401,6 +405,17 @@ def main():
         run(k)
     torch.cuda.synchronize()
     if not verdict_ok():
+        if world > 1 and cfg in ("C2", "C4", "C5"):  # which side is wrong: each slot's own partial
+            for sl in range(len(d_part)):
+                vo = torch.full((nb,), -1, dtype=torch.int32, device=dev)
+                L.gbls_final_verify_partials_device(ptr(d_part[sl]), ptr(d_err[sl]), 1, nb, ptr(vo), cur_stream())
+                vg = torch.full((nb,), -1, dtype=torch.int32, device=dev)
+                L.gbls_final_verify_partials_device(ptr(d_parts[sl]), ptr(d_errs[sl]), world, nb, ptr(vg), cur_stream())
+                torch.cuda.synchronize()
+                print("rank %d slot %d: verdict %s own-partial %s err %s gathered-again %s parts-equal-own %s" % (
+                    rank, sl, d_verdicts[sl].tolist(), vo.tolist(), d_err[sl].tolist(), vg.tolist(),
+                    bool(torch.equal(d_parts[sl][rank * nb * 576:(rank + 1) * nb * 576], d_part[sl]))),
+                    file=sys.stderr, flush=True)
         raise SystemExit("verdicts of the warm-up step are WRONG")
 
     L.gbls_profile_reset()

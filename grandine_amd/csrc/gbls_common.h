@@ -29,7 +29,10 @@ constexpr uint32_t kRowRegimeMax = 6144;
 #define GBLS_W4_MAX 1024
 #endif
 constexpr uint32_t kW4Max = GBLS_W4_MAX;
-constexpr uint32_t kRowClearMax = 4096;  // cofactor clearing on rows (up to one C2 batch)
+// cofactor clearing on rows up to this many points (4096 -> 2048 in r04: a single 4096-set batch
+// runs 802k sets/s with quad gangs vs 772k with rows, a C4 epoch of 2048-set launches 540k with
+// rows vs 480k with quad gangs; profiles/r04/q_*)
+constexpr uint32_t kRowClearMax = 2048;
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
 extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic (GBLS_ML_R28)
 // line-coefficient buffer bound per submission (19.6 KB per pair: 4 GB = 214k pairs,
