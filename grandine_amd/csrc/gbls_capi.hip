@@ -1727,6 +1727,11 @@ int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t 
         return fail(GBLS_ERR_HIP), FAILED;
       if (d.reg.p) (void)hipFree(d.reg.p);
       d.reg = nb;
+      // hipMemset / hipMemcpy go to the null stream and may still be running when they
+      // return; the decompression below runs on a context stream that does not wait for
+      // it, so a late memset could zero freshly decoded keys (seen as BAD_ENCODING segment
+      // flags in the first steps of two-process runs)
+      if (hipDeviceSynchronize() != hipSuccess) return fail(GBLS_ERR_HIP), FAILED;
     }
   }
   if (n) {

@@ -54,14 +54,6 @@ def test_bench_two_rank_c4_epoch_strong_scaling():
     args = [os.path.join(ROOT, "bench.py"), "--config", "C4", "--gpus", "2", "--steps", "2", "--warmup", "1",
             "--no-cpu"]
     r = _run(args, 600)
-    if r.returncode != 0 and "verdicts of the warm-up step are WRONG" in r.stderr:
-        # KNOWN OPEN ISSUE: in roughly 1 of 5 runs of this two-process
-        # flow on ONE GPU a warm-up step's gathered verdict is wrong (0 of 6 in a dedicated
-        # loop, profiles/r04/r_*); the bench prints each slot's own-partial verdict to stderr.
-        # One rerun, and the first failure stays visible as a warning.
-        import warnings
-        warnings.warn("2-rank C4 warm-up verdict wrong, rerunning once: " + r.stderr[-1500:])
-        r = _run(args, 600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0, line
