@@ -591,8 +591,69 @@ def bench_c1(args, L, G, F, np):
             out.append(time.perf_counter() - t)
         return sorted(out)
 
+    # the Rust drop-in's form (rust/bls_patch/verifier.rs): deferred Triple key LISTS handed over
+    # as points + per-set offsets, summed on the device inside the same submission
+    pts = F.public_keys([sks[int(i)] for i in idx])
+
+    def finish_points():
+        st = G.i32_array(n)
+        return L.gbls_multi_verify_compressed_ex(msgs, comp_sigs, pts, None, poff,
+                                                 (ctypes.c_uint64 * n)(*rands), n, st, 0)
+
     lat = timed(finish)
     lat2 = timed(finish_two_calls)
+    latp = timed(finish_points)
+    # single checks at n = 1 (SingleVerifier, sync-committee messages and contributions):
+    # Signature::verify, fast_aggregate_verify over 512 keys, a decompression, and
+    # SingleVerifier::extend of one triple (decompression + verify in one submission)
+    sm, ss, sp, _ = F.c2_batch(1, seed=65)
+    scomp = ctypes.create_string_buffer(96)
+    G.check(L.gbls_g2_compress(ss, 1, scomp), "compress")
+    fav_keys = pts[96 * int(off[2]):96 * int(off[3])]
+    fav_sig = sigs[192 * 2:192 * 3]
+    one = G.u32_array([0, 1])
+
+    def v1():
+        return L.gbls_verify(ss, sm, 32, sp)
+
+    def fav1():
+        return L.gbls_fast_aggregate_verify(fav_sig, msgs[64:96], 32, fav_keys, 512)
+
+    def dec1():
+        out, st = ctypes.create_string_buffer(192), G.i32_array(1)
+        rc = L.gbls_g2_decompress(scomp, 1, out, st)
+        return rc if st[0] == 0 else 1
+
+    def ext1():
+        st, v = G.i32_array(1), G.i32_array(1)
+        G.check(L.gbls_verify_batch_compressed(sm, scomp, sp, one, 1, st, v), "extend")
+        return v[0] if st[0] == 0 else 1
+
+    single = {name: timed(fn) for name, fn in (("verify", v1), ("fast_aggregate_verify_512", fav1),
+                                               ("g2_decompress", dec1), ("single_verifier_extend_1", ext1))}
+    # 16 threads of single verifies for 2 s (coalesced into shared submissions)
+    sv_calls = [0] * 16
+    sv_errs = []
+    sv_go = threading.Event()
+    sv_end = [0.0]
+
+    def sv_worker(k):
+        sv_go.wait()
+        while True:
+            if v1() != G.SUCCESS:
+                sv_errs.append(1)
+            if time.perf_counter() > sv_end[0]:
+                break
+            sv_calls[k] += 1
+
+    ths = [threading.Thread(target=sv_worker, args=(k,)) for k in range(16)]
+    for x in ths:
+        x.start()
+    sv_end[0] = time.perf_counter() + 2.0
+    sv_go.set()
+    for x in ths:
+        x.join()
+    assert not sv_errs
     # gossip: 64 single-key sets per call
     gm, gs, gp, gr = F.c2_batch(64, seed=64)
     r64 = (ctypes.c_uint64 * 64)(*gr)
@@ -662,6 +723,12 @@ def bench_c1(args, L, G, F, np):
                                    "included" % (n, int(off[-1])), "config": "C1"},
             "p99_ms": round(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3, 3),
             "decompress_then_verify_p50_ms": round(lat2[len(lat2) // 2] * 1e3, 3),
+            "points_pk_off": {"p50_ms": round(latp[len(latp) // 2] * 1e3, 3),
+                              "p99_ms": round(latp[min(len(latp) - 1, int(len(latp) * 0.99))] * 1e3, 3),
+                              "form": "the Rust drop-in's deferred Triple key lists: %d affine keys (96 B each) + "
+                                      "per-set offsets, summed on the device in the same submission" % int(off[-1])},
+            "single_checks_n1_p50_ms": {k: round(v[len(v) // 2] * 1e3, 3) for k, v in single.items()},
+            "single_verify_16_threads_per_s": round(sum(sv_calls) / 2.0, 1),
             "gossip64": {"p50_ms": round(glat[len(glat) // 2] * 1e3, 3),
                          "p99_ms": round(glat[min(len(glat) - 1, int(len(glat) * 0.99))] * 1e3, 3),
                          "concurrent_16_threads_sets_per_s": round(sum(done_calls) * 64 / conc, 1),

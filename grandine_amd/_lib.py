@@ -30,6 +30,7 @@ if _override:
 # tuning environment variables call enable_tuning() before the first lib() call.
 INIT_TUNING = 0x200
 INIT_PER_CHECK = 0x400  # grouped single checks off (deterministic per-check verdicts)
+INIT_NO_COALESCE = 0x100  # cross-caller coalescing off
 _tuning = False
 
 
@@ -56,6 +57,7 @@ FP12_BYTES = 576
 
 EXPORTS = [
     "gbls_init",
+    "gbls_set_policy",
     "gbls_last_error",
     "gbls_version",
     "gbls_device_count",
@@ -82,6 +84,7 @@ EXPORTS = [
     "gbls_verify",
     "gbls_fast_aggregate_verify",
     "gbls_aggregate_verify_batch",
+    "gbls_verify_batch_compressed",
     "gbls_fast_aggregate_verify_batch",
     "gbls_multi_verify",
     "gbls_multi_verify_segments",
@@ -136,6 +139,7 @@ def load_library():
             lib = _c.CDLL(LIB_PATH)
             sig = {
                 "gbls_init": (_c.c_int, [_c.c_uint32, _c.c_uint32]),
+                "gbls_set_policy": (_c.c_uint32, [_c.c_uint32]),
                 "gbls_last_error": (_c.c_int, []),
                 "gbls_version": (_c.c_char_p, []),
                 "gbls_device_count": (_c.c_int, []),
@@ -165,6 +169,7 @@ def load_library():
                 "gbls_verify": (_c.c_int, [_vp, _vp, _sz, _vp]),
                 "gbls_fast_aggregate_verify": (_c.c_int, [_vp, _vp, _sz, _vp, _sz]),
                 "gbls_aggregate_verify_batch": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
+                "gbls_verify_batch_compressed": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp]),
                 "gbls_fast_aggregate_verify_batch": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
                 "gbls_multi_verify": (_c.c_int, [_vp, _vp, _vp, _vp, _sz]),
                 "gbls_multi_verify_segments": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp]),

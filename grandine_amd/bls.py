@@ -249,25 +249,58 @@ class Signature:
 
     @staticmethod
     def multi_verify_compressed(messages: Iterable[bytes], signature_bytes: Iterable[bytes],
-                                public_keys: Iterable[PublicKey], randoms: Sequence[int] = None) -> int:
+                                public_keys: Iterable, randoms: Sequence[int] = None,
+                                call_flags: int = 0) -> int:
         """MultiVerifier::finish's decompress + multi_verify (verifier.rs:301-323) as one device
-        submission (gbls_multi_verify_compressed): 0 = valid, 5 = VERIFY_FAIL, otherwise the
-        first signature's decompression status (finish's Err(DecompressionFailed))."""
+        submission (gbls_multi_verify_compressed_ex): 0 = valid, 5 = VERIFY_FAIL, otherwise the
+        first signature's decompression status (finish's Err(DecompressionFailed)).  Each set's
+        key is a PublicKey or a list of them, summed on the device inside the same submission
+        (a deferred Triple::verify_aggregate, verifier.rs:387-405)."""
         msgs = [bytes(m) for m in messages]
         sigs = [bytes(s) for s in signature_bytes]
-        pks = list(public_keys)
+        keys = [list(k) if isinstance(k, (list, tuple)) else [k] for k in public_keys]
         n = len(sigs)
-        if n == 0 or len(msgs) != n or len(pks) != n:
+        if n == 0 or len(msgs) != n or len(keys) != n:
             return G.VERIFY_FAIL
         if any(len(m) != 32 for m in msgs) or any(len(s) != 96 for s in sigs):
             raise ValueError("messages must be 32-byte signing roots and signatures 96 bytes")
         if randoms is None:
             randoms = [secrets.randbits(64) or 1 for _ in range(n)]
+        off = [0]
+        for k in keys:
+            off.append(off[-1] + len(k))
         L = G.lib()
         st = G.i32_array(n)
-        return L.gbls_multi_verify_compressed(G.buf(b"".join(msgs)), G.buf(b"".join(sigs)),
-                                              G.buf(b"".join(p.raw for p in pks)), None, None,
-                                              G.u64_array(randoms), n, st)
+        return L.gbls_multi_verify_compressed_ex(
+            G.buf(b"".join(msgs)), G.buf(b"".join(sigs)), G.buf(b"".join(p.raw for k in keys for p in k)),
+            None, G.u32_array(off), G.u64_array(randoms), n, st, call_flags)
+
+    @staticmethod
+    def verify_batch_compressed(messages: Iterable[bytes], signature_bytes: Iterable[bytes],
+                                public_keys: Iterable) -> List:
+        """SingleVerifier::extend's try_from + verify per triple (verifier.rs:215-236) as ONE
+        coalesced device submission (gbls_verify_batch_compressed).  Per check: a decompression
+        status (0 = decoded, else its BLST_ERROR) and whether it verifies; keys as in
+        multi_verify_compressed (a list = fast_aggregate_verify over it)."""
+        msgs = [bytes(m) for m in messages]
+        sigs = [bytes(s) for s in signature_bytes]
+        keys = [list(k) if isinstance(k, (list, tuple)) else [k] for k in public_keys]
+        n = len(sigs)
+        if len(msgs) != n or len(keys) != n:
+            raise ValueError("one message and one key set per signature")
+        if n == 0:
+            return []
+        if any(len(m) != 32 for m in msgs) or any(len(s) != 96 for s in sigs):
+            raise ValueError("messages must be 32-byte signing roots and signatures 96 bytes")
+        off = [0]
+        for k in keys:
+            off.append(off[-1] + len(k))
+        L = G.lib()
+        st, v = G.i32_array(n), G.i32_array(n)
+        G.check(L.gbls_verify_batch_compressed(
+            G.buf(b"".join(msgs)), G.buf(b"".join(sigs)), G.buf(b"".join(p.raw for k in keys for p in k) or bytes(96)),
+            G.u32_array(off), n, st, v), "gbls_verify_batch_compressed")
+        return [(st[i], v[i] == G.SUCCESS) for i in range(n)]
 
     def __eq__(self, other):
         return isinstance(other, Signature) and self.raw == other.raw

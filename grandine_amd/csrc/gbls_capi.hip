@@ -140,6 +140,11 @@ struct Ctx {
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
              ev_done = nullptr, ev_upl = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool done_pending = false, upl_pending = false;
+  // recorded behind this context's last kernel that read the validator registry (written under
+  // the shared registry lock, read by gbls_registry_set under the exclusive one): a grown
+  // registry's old table is freed only after every such reader
+  hipEvent_t ev_reg = nullptr;
+  bool reg_read = false;
   int cls = 0;                        // 0: normal, 1: block import (every stream high priority)
   bool active = false;                // a call holds the lease and has begun
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
@@ -179,6 +184,7 @@ struct Ctx {
     HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_upl, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_reg, hipEventDisableTiming));
     return true;
   }
   // CU-masked stream triple: mode 1 = main chain on the first `main_cus` CUs, sides on the
@@ -287,7 +293,16 @@ struct Device {
   uint32_t nsimd = 1024;  // 4 SIMDs per CU
   int ncu = 256;
   sched::CtxPool<Ctx> pool;  // per-class capped context pool (gbls_sched.h)
-  Buf reg;  // validator registry (replica), guarded by Engine::reg_mu
+  // validator registry (replica), guarded by Engine::reg_mu.  Every write (growth, zeroing,
+  // decompression, replica copies) is stream-ordered on reg_st; reg_ev follows the last one and
+  // every registry reader's stream waits on it (GPU-side) before its gather.  A grown table's
+  // old buffer is freed on retire_st behind its readers (Ctx::ev_reg), never by a host wait.
+  Buf reg;
+  bool reg_pooled = false;  // reg.p from hipMallocAsync (freed by hipFreeAsync)
+  std::vector<void *> reg_kept;  // old tables kept when stream-ordered allocation is missing
+  hipStream_t reg_st = nullptr, retire_st = nullptr;
+  hipEvent_t reg_ev = nullptr, reg_tmp = nullptr;
+  bool reg_ev_set = false;
 };
 
 struct Engine {
@@ -353,9 +368,11 @@ class Lease {
 
 bool engine_init(uint32_t device_mask, uint32_t flags) {
   std::lock_guard<std::mutex> lk(g.mu);
-  // policy flags apply on every call, also to an engine that is already open
-  g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
-  g.per_check.store((flags & GBLS_INIT_PER_CHECK) != 0);
+  // policy flags are sticky: a gbls_init that names one turns it on, also on an engine that is
+  // already open, and no later gbls_init turns it off (a library's lazy gbls_init(mask, 0) must
+  // not undo an operator's or a spec-test harness's choice); gbls_set_policy sets them outright
+  if (flags & GBLS_INIT_NO_COALESCE) g.coalesce.store(false);
+  if (flags & GBLS_INIT_PER_CHECK) g.per_check.store(true);
   if (g.ready.load()) return true;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GBLS_ERR_NO_DEVICE);
@@ -445,6 +462,20 @@ bool valid_offsets(const uint32_t *off, size_t nseg, size_t n) {
 // pointers in a coalescer request)
 using PkSource = sched::KeySource<g1a>;
 
+// A kernel reading the registry on stream st: first wait (on the GPU) for the registry's
+// pending writes, afterwards mark the read so that a growth retires the old table behind it.
+// Both under the shared registry lock.
+bool registry_read_begin(Ctx &c, Device &d, hipStream_t st) {
+  (void)c;
+  if (d.reg_ev_set) HIPCHK(hipStreamWaitEvent(st, d.reg_ev, 0));
+  return true;
+}
+bool registry_read_end(Ctx &c, hipStream_t st) {
+  HIPCHK(hipEventRecord(c.ev_reg, st));
+  c.reg_read = true;
+  return true;
+}
+
 // Resolve a DEVICE key source into per-set affine keys on stream st; *pre = per-set
 // status (nonzero = reject: empty aggregate, index out of range) or nullptr.  The caller
 // holds the registry lock (shared) while it enqueues.
@@ -459,6 +490,7 @@ bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t s
   if (!c.ensure(c.pks, n * sizeof(g1a)) || !c.ensure(c.pre, n * sizeof(int32_t))) return false;
   StageTimer t(S_PK_GATHER, st);
   const g1a *reg = d.reg.as<g1a>();
+  if (src.idx && !registry_read_begin(c, d, st)) return false;
   if (src.pts)
     launch_g1_aggregate_seg(st, src.pts, src.off, (uint32_t)n, c.pks.as<g1a>(),
                             c.pre.as<int32_t>());
@@ -468,6 +500,7 @@ bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t s
   else
     launch_g1_gather_idx(st, reg, (uint32_t)g.reg_n, src.idx, (uint32_t)n, c.pks.as<g1a>(),
                          c.pre.as<int32_t>());
+  if (src.idx && !registry_read_end(c, st)) return false;
   *pks = c.pks.as<g1a>();
   *pre = c.pre.as<int32_t>();
   return true;
@@ -741,6 +774,11 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     // sigs is then the lease's own output buffer (c.sigd, enqueue_host_batch)
     launch_g2_decompress(side2, c.sig_c, N, const_cast<g2a *>(sigs), c.sig_st);
     pre2 = c.sig_st;
+    if (sig_groupcheck) {  // single checks (SingleVerifier::extend): decoding AND subgroup
+      HIPCHK(hipMemcpyAsync(c.pre2.p, c.sig_st, (size_t)N * 4, hipMemcpyDeviceToDevice, side2));
+      launch_g2_check(side2, sigs, N, c.pre2.as<int32_t>(), 1);
+      pre2 = c.pre2.as<int32_t>();
+    }
     c.sig_c = nullptr;
     c.sig_st = nullptr;
   } else if (sig_groupcheck) {
@@ -966,7 +1004,8 @@ bool upload_pks(Ctx &c, const PkSource &host, size_t b, size_t e, hipStream_t st
 // One device: host batch [sets b..e) in segments seg (rebased, host) -> per-segment
 // verdicts (host) when `verdicts`, or else the Miller partial + error flag of the single
 // segment, copied device-to-device (hipMemcpyPeerAsync, xGMI) to part_dst / err_dst on
-// device dst_dev.  Enqueues only; the caller synchronises `c.own` (or waits on it).
+// device dst_dev.  rands == nullptr: independent single checks (r_i = 1, signature subgroup
+// check, one segment per set).  Enqueues only; the caller synchronises `c.own` (or waits on it).
 bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
                         const uint8_t *sigs_c, int32_t *sig_status, const PkSource &src,
                         const uint64_t *rands, size_t b, size_t e, const uint32_t *seg,
@@ -975,8 +1014,9 @@ bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
   hipStream_t st = c.own;
   size_t n = e - b;
   if (!c.begin(st)) return false;
+  const bool single = rands == nullptr;
   if (!c.upload_staged(c.in0, msgs + 32 * b, 32 * n, st) ||
-      !c.upload_staged(c.in3, rands + b, n * 8, st))
+      (!single && !c.upload_staged(c.in3, rands + b, n * 8, st)))
     return false;
   const g2a *dsigs;
   if (sigs_c) {  // compressed: decompressed on the device by the pipeline (side stream 2)
@@ -997,14 +1037,15 @@ bool enqueue_host_batch(Ctx &c, Device &d, const uint8_t *msgs, const g2a *sigs,
     return false;
   }
   bool ok;
+  const uint64_t *drands = single ? nullptr : c.in3.as<uint64_t>();
   if (verdicts)
     ok = c.ensure(c.out1, nseg * sizeof(int32_t)) &&
-         pipeline_verdicts(c, d, c.in0.as<uint8_t>(), nullptr, dsigs, dsrc, c.in3.as<uint64_t>(),
-                           false, n, seg, nseg, c.out1.as<int32_t>(), st);
+         pipeline_verdicts(c, d, c.in0.as<uint8_t>(), nullptr, dsigs, dsrc, drands, single, n, seg,
+                           nseg, c.out1.as<int32_t>(), st);
   else
     ok = c.ensure(c.part, sizeof(fp12)) && c.ensure(c.err, 16) &&
-         pipeline_partials(c, d, c.in0.as<uint8_t>(), nullptr, dsigs, dsrc, c.in3.as<uint64_t>(),
-                           false, n, seg, 1, 0, c.part.as<fp12>(), c.err.as<int32_t>(), st);
+         pipeline_partials(c, d, c.in0.as<uint8_t>(), nullptr, dsigs, dsrc, drands, single, n, seg,
+                           1, 0, c.part.as<fp12>(), c.err.as<int32_t>(), st);
   c.sig_c = nullptr;  // the option is for this call only, consumed or not
   c.sig_st = nullptr;
   if (!ok) return false;
@@ -1029,7 +1070,7 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
   // ---- one large batch: per-device Miller partials, gathered device-to-device onto device 0
   // (hipMemcpyPeerAsync over xGMI, ordered by events, no host round trip), one final
   // exponentiation there
-  if (nseg == 1 && ndev > 1 && n >= 2 * kShardMinSets) {
+  if (nseg == 1 && ndev > 1 && n >= 2 * kShardMinSets && rands) {
     size_t k = std::min(ndev, n / kShardMinSets);
     Device &d0 = *g.devs[0];
     Lease L0(d0, cls);
@@ -1069,6 +1110,7 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
                               L0->out1.as<int32_t>(), st0);
     if (ok && hipMemcpyAsync(verdicts, L0->out1.p, 4, hipMemcpyDeviceToHost, st0) != hipSuccess)
       ok = fail(GBLS_ERR_HIP);
+    rl.unlock();  // enqueued: the host wait does not hold up registry updates
     // the final's stream waited on every shard, so its completion covers theirs (including the
     // shards' signature-status copies to the host); on a failure every shard is drained
     if (ok && hipStreamSynchronize(st0) != hipSuccess) ok = fail(GBLS_ERR_HIP);
@@ -1102,6 +1144,7 @@ bool verify_host(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c, in
     ok = L.ok() && enqueue_host_batch(*L, d, msgs, sigs, sigs_c, sig_status, src, rands, b, e,
                                       segs[j].data(), s1 - s0, verdicts + s0, nullptr, nullptr, 0);
   }
+  rl.unlock();  // enqueued: the host waits do not hold up registry updates
   for (auto &L : leases)
     if (hipStreamSynchronize((*L)->own) != hipSuccess) ok = fail(GBLS_ERR_HIP);
   return ok;
@@ -1206,6 +1249,52 @@ bool bisect_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
   return true;
 }
 
+// the registry's streams and events on device d (created on first use, under reg_mu)
+bool registry_streams(Device &d) {
+  if (d.reg_st) return true;
+  HIPCHK(hipSetDevice(d.hipdev));
+  HIPCHK(hipStreamCreateWithFlags(&d.reg_st, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&d.retire_st, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&d.reg_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.reg_tmp, hipEventDisableTiming));
+  return true;
+}
+// Grow d's table to hold `need` bytes, stream-ordered on d.reg_st: a new table (zeroed past the
+// loaded entries, the loaded ones copied), and the old one freed on d.retire_st once the copy
+// and every kernel that read it have run (each context's last registry read, and the replica
+// copies of earlier updates).  No host wait, no device synchronisation.
+bool registry_grow(Device &d, size_t need, size_t loaded) {
+  const size_t want = need + need / 4;
+  void *nb = nullptr;
+  bool pooled = true;
+  if (hipMallocAsync(&nb, want, d.reg_st) != hipSuccess) {  // no stream-ordered allocator
+    (void)hipGetLastError();
+    pooled = false;
+    HIPCHK(hipMalloc(&nb, want));
+  }
+  if (loaded) HIPCHK(hipMemcpyAsync(nb, d.reg.p, loaded, hipMemcpyDeviceToDevice, d.reg_st));
+  HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nb) + loaded, 0, want - loaded, d.reg_st));
+  if (d.reg.p) {
+    if (d.reg_pooled) {
+      HIPCHK(hipEventRecord(d.reg_tmp, d.reg_st));
+      HIPCHK(hipStreamWaitEvent(d.retire_st, d.reg_tmp, 0));
+      bool ok = true;
+      d.pool.for_each([&](Ctx &c) {
+        if (c.reg_read && hipStreamWaitEvent(d.retire_st, c.ev_reg, 0) != hipSuccess) ok = false;
+      });
+      for (auto &o : g.devs)  // replica copies of earlier updates read device 0's table
+        if (o->reg_ev_set && hipStreamWaitEvent(d.retire_st, o->reg_ev, 0) != hipSuccess) ok = false;
+      if (!ok) return fail(GBLS_ERR_HIP);
+      HIPCHK(hipFreeAsync(d.reg.p, d.retire_st));
+    } else {
+      d.reg_kept.push_back(d.reg.p);  // readers may still be running: kept, never host-waited
+    }
+  }
+  d.reg.p = nb;
+  d.reg.cap = want;
+  d.reg_pooled = pooled;
+  return true;
+}
 }  // namespace
 
 #define API_BEGIN                   \
@@ -1217,6 +1306,14 @@ extern "C" {
 int gbls_init(uint32_t device_mask, uint32_t flags) {
   t_last_error = GBLS_ERR_NONE;
   return engine_init(device_mask, flags) ? GBLS_SUCCESS : FAILED;
+}
+
+uint32_t gbls_set_policy(uint32_t flags) {
+  uint32_t prev = (g.coalesce.load() ? 0u : GBLS_INIT_NO_COALESCE) |
+                  (g.per_check.load() ? GBLS_INIT_PER_CHECK : 0u);
+  g.coalesce.store((flags & GBLS_INIT_NO_COALESCE) == 0);
+  g.per_check.store((flags & GBLS_INIT_PER_CHECK) != 0);
+  return prev;
 }
 
 int gbls_last_error(void) { return t_last_error; }
@@ -1338,13 +1435,18 @@ static int aggregate_impl(const void *pts, const uint32_t *idx, const uint32_t *
   else if (which == 2)
     launch_g2_aggregate_seg(st, c.in0.as<g2a>(), c.in1.as<uint32_t>(), (uint32_t)nseg,
                             c.out0.as<g2a>(), c.out1.as<int32_t>());
+  else if (!registry_read_begin(c, d, st))
+    return FAILED;
   else
     launch_g1_aggregate_idx(st, d.reg.as<g1a>(), (uint32_t)g.reg_n, c.in0.as<uint32_t>(),
                             c.in1.as<uint32_t>(), (uint32_t)nseg, c.out0.as<g1a>(),
                             c.out1.as<int32_t>());
+  if (which == 3 && !registry_read_end(c, st)) return FAILED;
   if (hipMemcpyAsync(out, c.out0.p, nseg * psz, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(status, c.out1.p, nseg * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
+      hipMemcpyAsync(status, c.out1.p, nseg * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    return fail(GBLS_ERR_HIP), FAILED;
+  rl.unlock();  // enqueued: the host wait below does not hold up registry updates
+  if (hipStreamSynchronize(st) != hipSuccess) {
     fill(status, nseg, GBLS_AGGR_TYPE_MISMATCH);
     return fail(GBLS_ERR_HIP), FAILED;
   }
@@ -1425,17 +1527,59 @@ static int single_checks(const g2a *sigs, const uint8_t *msg_data, const uint32_
   if (!pipeline_verdicts(c, d, c.in1.as<uint8_t>(), c.in2.as<uint32_t>(), c.in0.as<g2a>(), src,
                          nullptr, true, m, ident.data(), m, c.out1.as<int32_t>(), st))
     return FAILED;
-  if (hipMemcpyAsync(verdicts, c.out1.p, m * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
+  if (hipMemcpyAsync(verdicts, c.out1.p, m * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    return fail(GBLS_ERR_HIP), FAILED;
+  rl.unlock();  // enqueued: the host wait does not hold up registry updates
+  if (hipStreamSynchronize(st) != hipSuccess) {
     fill(verdicts, m, GBLS_VERIFY_FAIL);
     return fail(GBLS_ERR_HIP), FAILED;
   }
   return GBLS_SUCCESS;
 }
 
+// Single checks with 32-byte messages (every consensus caller: signing roots) go through the
+// coalescer (f3): concurrent Signature::verify / fast_aggregate_verify calls -- sync-committee
+// messages and contributions (operation_pools/src/sync_committee_agg_pool/tasks.rs:397-430),
+// SingleVerifier::extend (helper_functions/src/verifier.rs:215-236) on many rayon workers --
+// become segments of ONE submission instead of one pipeline each.  Signatures are points
+// (sigs) or 96-byte encodings (sigs_c, decompressed in the same submission, statuses in
+// sig_status: SingleVerifier::extend's try_from and verify cost one submission, not two).
+// Keys: one point per check, or the sum of pks[pk_off[i] .. pk_off[i+1]) (fast_aggregate_verify).
+static int single_checks_co(const uint8_t *msgs, const g2a *sigs, const uint8_t *sigs_c,
+                            int32_t *sig_status, const g1a *pks, const uint32_t *pk_off, size_t m,
+                            int32_t *verdicts) {
+  fill(verdicts, m, GBLS_VERIFY_FAIL);
+  if (sig_status) fill(sig_status, m, GBLS_BAD_ENCODING);
+  API_BEGIN
+  if (m == 0) return GBLS_SUCCESS;
+  if (!msgs || !pks || (!sigs == !sigs_c) || (sigs_c && !sig_status)) return fail(GBLS_ERR_ARG), FAILED;
+  if (pk_off && !valid_offsets(pk_off, m, pk_off[m])) return fail(GBLS_ERR_ARG), FAILED;
+  std::vector<uint32_t> ident(m + 1);
+  for (size_t i = 0; i <= m; i++) ident[i] = (uint32_t)i;
+  CoReq r{msgs, sigs, PkSource(), nullptr, m, ident.data(), m, verdicts};
+  r.src.pts = pks;
+  r.src.off = pk_off;
+  r.sigs_c = sigs_c;
+  r.sig_status = sig_status;
+  if (!coalesced_verify(r)) {
+    fill(verdicts, m, GBLS_VERIFY_FAIL);
+    if (sig_status) fill(sig_status, m, GBLS_BAD_ENCODING);
+    return FAILED;
+  }
+  return GBLS_SUCCESS;
+}
+static bool msgs_are_roots(const uint32_t *msg_off, size_t m) {
+  for (size_t i = 0; i <= m; i++)
+    if (msg_off[i] != 32 * i) return false;
+  return true;
+}
+
 int gbls_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                 const uint32_t *msg_off, const gbls_p1_affine *pks, size_t m,
                                 int32_t *verdicts) {
+  if (m && msg_off && msgs_are_roots(msg_off, m))
+    return single_checks_co(msg_data, reinterpret_cast<const g2a *>(sigs), nullptr, nullptr,
+                            reinterpret_cast<const g1a *>(pks), nullptr, m, verdicts);
   return single_checks(reinterpret_cast<const g2a *>(sigs), msg_data, msg_off, pks, nullptr, m, 0,
                        verdicts);
 }
@@ -1453,8 +1597,18 @@ int gbls_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
 int gbls_fast_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                      const uint32_t *msg_off, const gbls_p1_affine *pks,
                                      const uint32_t *seg_off, size_t m, int32_t *verdicts) {
+  if (m && msg_off && msgs_are_roots(msg_off, m))
+    return single_checks_co(msg_data, reinterpret_cast<const g2a *>(sigs), nullptr, nullptr,
+                            reinterpret_cast<const g1a *>(pks), seg_off, m, verdicts);
   return single_checks(reinterpret_cast<const g2a *>(sigs), msg_data, msg_off, pks, seg_off, m, 1,
                        verdicts);
+}
+
+int gbls_verify_batch_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
+                                 const gbls_p1_affine *pks, const uint32_t *pk_off, size_t m,
+                                 int32_t *sig_status, int32_t *verdicts) {
+  return single_checks_co(msgs ? &msgs[0][0] : nullptr, nullptr, sigs ? &sigs[0][0] : nullptr,
+                          sig_status, reinterpret_cast<const g1a *>(pks), pk_off, m, verdicts);
 }
 
 int gbls_fast_aggregate_verify_indexed(const gbls_p2_affine *sigs, const uint8_t *msg_data,
@@ -1532,7 +1686,7 @@ int gbls_multi_verify_compressed_ex(const uint8_t (*msgs)[32], const uint8_t (*s
   fill(sig_status, n, GBLS_BAD_ENCODING);
   API_BEGIN
   if (n == 0) return GBLS_VERIFY_FAIL;
-  if (!pks == !pk_idx || (pks && pk_off)) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
+  if (!pks == !pk_idx) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
   if (pk_off && !valid_offsets(pk_off, n, pk_off[n])) return fail(GBLS_ERR_ARG), GBLS_VERIFY_FAIL;
   uint32_t off[2] = {0, (uint32_t)n};
   int32_t v = GBLS_VERIFY_FAIL;
@@ -1703,63 +1857,95 @@ int gbls_fast_aggregate_verify_indexed_device(const gbls_p2_affine *sigs, const 
 // size is committed only when every replica holds the slice; a failure part-way truncates
 // the registry to `first`, so no index can resolve to replicas that disagree (indices past
 // the size are BAD_ENCODING everywhere).
+
+// ---- validator registry (f1): bulk decompress + validate on the device, replicated.
+// The keys are decompressed ONCE (on the first engine device) and the 96-B affine table
+// slice is copied device-to-device to every other replica (hipMemcpyPeerAsync over xGMI
+// between GPUs), so 8 GPUs cost one decompression of the registry, not eight.  Every write is
+// enqueued under the exclusive registry lock on the devices' registry streams; verifications
+// already in flight keep running (a growth frees the old table behind them, on the GPU), later
+// ones wait for the update on the GPU, and the host wait for the statuses happens after the
+// lock is released.  A failure truncates the registry to `first`, so no index can resolve to
+// replicas that disagree (indices past the size are BAD_ENCODING everywhere).
 int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t *status) {
   fill(status, n, GBLS_BAD_ENCODING);
   API_BEGIN
-  std::unique_lock<std::shared_mutex> wl(g.reg_mu);
-  size_t new_n = std::max(g.reg_n, first + n);
-  if (new_n > 0xffffffffull) return fail(GBLS_ERR_ARG), FAILED;
-  auto broken = [&]() {
+  std::vector<int32_t> st0(n);
+  std::vector<hipEvent_t> done;
+  struct EvGuard {
+    std::vector<hipEvent_t> &v;
+    ~EvGuard() {
+      for (hipEvent_t e : v) (void)hipEventDestroy(e);
+    }
+  } guard{done};
+  auto broken = [&](std::unique_lock<std::shared_mutex> &wl) {
+    if (!wl.owns_lock()) wl.lock();
     g.reg_n = std::min(g.reg_n, first);
     fill(status, n, GBLS_BAD_ENCODING);
     return FAILED;
   };
-  for (size_t j = 0; j < g.devs.size(); j++) {
-    Device &d = *g.devs[j];
-    if (hipSetDevice(d.hipdev) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-      return fail(GBLS_ERR_HIP), FAILED;
-    if (new_n * sizeof(g1a) > d.reg.cap) {  // grow, keeping the entries already loaded
-      Buf nb;
-      if (!nb.ensure(new_n * sizeof(g1a))) return fail(GBLS_ERR_HIP), FAILED;
-      if (hipMemset(nb.p, 0, nb.cap) != hipSuccess) return fail(GBLS_ERR_HIP), FAILED;
-      if (g.reg_n && hipMemcpy(nb.p, d.reg.p, g.reg_n * sizeof(g1a), hipMemcpyDeviceToDevice) !=
-                         hipSuccess)
-        return fail(GBLS_ERR_HIP), FAILED;
-      if (d.reg.p) (void)hipFree(d.reg.p);
-      d.reg = nb;
-      // hipMemset / hipMemcpy go to the null stream and may still be running when they
-      // return; the decompression below runs on a context stream that does not wait for
-      // it, so a late memset could zero freshly decoded keys (seen as BAD_ENCODING segment
-      // flags in the first steps of two-process runs)
-      if (hipDeviceSynchronize() != hipSuccess) return fail(GBLS_ERR_HIP), FAILED;
-    }
-  }
-  if (n) {
-    std::vector<int32_t> st0(n);
+  std::unique_lock<std::shared_mutex> wl(g.reg_mu);
+  {
+    const size_t new_n = std::max(g.reg_n, first + n);
+    if (new_n > 0xffffffffull) return fail(GBLS_ERR_ARG), FAILED;
     Device &d0 = *g.devs[0];
-    Lease L(d0);
-    Ctx &c = *L;
-    hipStream_t st = c.own;
-    if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &pks[0][0], 48 * n, st) ||
-        !c.ensure(c.out1, n * sizeof(int32_t)))
-      return broken();
-    g1a *slice0 = d0.reg.as<g1a>() + first;
-    launch_g1_decompress(st, c.in0.as<uint8_t>(), (uint32_t)n, 1, slice0, c.out1.as<int32_t>());
-    if (hipMemcpyAsync(st0.data(), c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
-      return fail(GBLS_ERR_HIP), broken();
-    // broadcast the decoded slice: queued on the same stream behind the decompression
-    for (size_t j = 1; j < g.devs.size(); j++) {
-      Device &d = *g.devs[j];
-      g1a *dst = d.reg.as<g1a>() + first;
-      hipError_t e = d.hipdev == d0.hipdev
-                         ? hipMemcpyAsync(dst, slice0, n * sizeof(g1a), hipMemcpyDeviceToDevice, st)
-                         : hipMemcpyPeerAsync(dst, d.hipdev, slice0, d0.hipdev, n * sizeof(g1a), st);
-      if (e != hipSuccess) return fail(GBLS_ERR_HIP), broken();
+    for (auto &dp : g.devs) {
+      Device &d = *dp;
+      if (!registry_streams(d) || hipSetDevice(d.hipdev) != hipSuccess) return fail(GBLS_ERR_HIP), broken(wl);
+      if (&d == &d0)  // earlier replica copies read device 0's table: overwrite it after them
+        for (auto &o : g.devs)
+          if (o.get() != &d0 && o->reg_ev_set && hipStreamWaitEvent(d0.reg_st, o->reg_ev, 0) != hipSuccess)
+            return fail(GBLS_ERR_HIP), broken(wl);
+      if (new_n * sizeof(g1a) > d.reg.cap) {
+        if (!registry_grow(d, new_n * sizeof(g1a), g.reg_n * sizeof(g1a))) return broken(wl);
+      } else if (first > g.reg_n &&  // a gap past the loaded keys: never-loaded slots are zero
+                 hipMemsetAsync(d.reg.as<g1a>() + g.reg_n, 0, (first - g.reg_n) * sizeof(g1a),
+                                d.reg_st) != hipSuccess) {
+        return fail(GBLS_ERR_HIP), broken(wl);
+      }
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(GBLS_ERR_HIP), broken();
-    std::memcpy(status, st0.data(), n * 4);
+    if (n) {
+      if (hipSetDevice(d0.hipdev) != hipSuccess) return fail(GBLS_ERR_HIP), broken(wl);
+      Lease L(d0);  // workspaces and staging; the work itself runs on the registry stream
+      Ctx &c = *L;
+      hipStream_t st = d0.reg_st;
+      if (!L.ok() || !c.begin(st) || !c.upload_staged(c.in0, &pks[0][0], 48 * n, st) ||
+          !c.ensure(c.out1, n * sizeof(int32_t)))
+        return broken(wl);
+      g1a *slice0 = d0.reg.as<g1a>() + first;
+      launch_g1_decompress(st, c.in0.as<uint8_t>(), (uint32_t)n, 1, slice0, c.out1.as<int32_t>());
+      if (hipMemcpyAsync(st0.data(), c.out1.p, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipEventRecord(d0.reg_tmp, st) != hipSuccess)
+        return fail(GBLS_ERR_HIP), broken(wl);
+      // replicas: each copies the decoded slice on its own registry stream, behind its growth
+      for (size_t j = 1; j < g.devs.size(); j++) {
+        Device &d = *g.devs[j];
+        g1a *dst = d.reg.as<g1a>() + first;
+        if (hipSetDevice(d.hipdev) != hipSuccess || hipStreamWaitEvent(d.reg_st, d0.reg_tmp, 0) != hipSuccess)
+          return fail(GBLS_ERR_HIP), broken(wl);
+        hipError_t e = d.hipdev == d0.hipdev
+                           ? hipMemcpyAsync(dst, slice0, n * sizeof(g1a), hipMemcpyDeviceToDevice, d.reg_st)
+                           : hipMemcpyPeerAsync(dst, d.hipdev, slice0, d0.hipdev, n * sizeof(g1a), d.reg_st);
+        if (e != hipSuccess) return fail(GBLS_ERR_HIP), broken(wl);
+      }
+    }
+    // later readers wait (on the GPU) for this update; this call waits on its own events
+    for (auto &dp : g.devs) {
+      Device &d = *dp;
+      hipEvent_t e = nullptr;
+      if (hipSetDevice(d.hipdev) != hipSuccess || hipEventRecord(d.reg_ev, d.reg_st) != hipSuccess ||
+          hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        return fail(GBLS_ERR_HIP), broken(wl);
+      done.push_back(e);
+      if (hipEventRecord(e, d.reg_st) != hipSuccess) return fail(GBLS_ERR_HIP), broken(wl);
+      d.reg_ev_set = true;
+    }
+    g.reg_n = new_n;
   }
-  g.reg_n = new_n;
+  wl.unlock();
+  for (hipEvent_t e : done)
+    if (hipEventSynchronize(e) != hipSuccess) return fail(GBLS_ERR_HIP), broken(wl);
+  if (n) std::memcpy(status, st0.data(), n * 4);
   return GBLS_SUCCESS;
 }
 

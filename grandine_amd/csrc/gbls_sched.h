@@ -80,6 +80,12 @@ struct CtxPool {
     std::lock_guard<std::mutex> lk(mu);
     return all.size();
   }
+  // f(ctx) for every context, leased or idle (under the pool mutex: f must not block)
+  template <class F>
+  void for_each(F &&f) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &c : all) f(*c);
+  }
 
  private:
   Ctx *take(size_t i) {
@@ -97,7 +103,9 @@ struct KeySource {
   const uint32_t *off = nullptr;  // per-set ranges [off[i], off[i+1]) of pts / idx
 };
 
-// One caller's batch (host pointers, borrowed for the call).
+// One caller's batch (host pointers, borrowed for the call).  rands == nullptr: independent
+// single checks (Signature::verify / fast_aggregate_verify semantics: r_i = 1, the
+// signature's subgroup check, one segment per set), merged only with other single checks.
 template <class G1, class G2>
 struct Request {
   using g1_type = G1;
@@ -115,7 +123,9 @@ struct Request {
   int prio = 0;                     // 1: block import
   bool done = false, ok = false;
   int err = 0;                      // the verifier's side-channel error code
-  int kind() const { return (src.pts ? 1 : 0) | (src.off ? 2 : 0) | (sigs_c ? 4 : 0); }
+  int kind() const {
+    return (src.pts ? 1 : 0) | (src.off ? 2 : 0) | (sigs_c ? 4 : 0) | (rands ? 0 : 8);
+  }
   size_t nkeys() const { return src.off ? src.off[n] : n; }
 };
 
@@ -152,11 +162,11 @@ void run_merged(std::vector<Req *> &batch, Verify &&verify) {
     nk += r->nkeys();
   }
   const Req &r0 = *batch[0];
-  const bool comp = r0.sigs_c != nullptr;
+  const bool comp = r0.sigs_c != nullptr, single = r0.rands == nullptr;
   std::vector<uint8_t> msgs(32 * n), sigc(comp ? 96 * n : 0);
   std::vector<G2> sigs(comp ? 0 : n);
   std::vector<int32_t> sst(comp ? n : 0, 1 /* BAD_ENCODING until decoded */);
-  std::vector<uint64_t> rands(n);
+  std::vector<uint64_t> rands(single ? 0 : n);
   std::vector<G1> pts;
   std::vector<uint32_t> idx, off, seg(nseg + 1);
   if (r0.src.pts)
@@ -173,7 +183,7 @@ void run_merged(std::vector<Req *> &batch, Verify &&verify) {
       std::memcpy(&sigc[96 * at], r->sigs_c, 96 * r->n);
     else
       std::memcpy(&sigs[at], r->sigs, r->n * sizeof(G2));
-    std::memcpy(&rands[at], r->rands, r->n * 8);
+    if (!single) std::memcpy(&rands[at], r->rands, r->n * 8);
     const size_t k = r->nkeys();
     if (r0.src.pts)
       std::memcpy(&pts[kat], r->src.pts, k * sizeof(G1));
@@ -186,8 +196,8 @@ void run_merged(std::vector<Req *> &batch, Verify &&verify) {
     sat += r->nseg;
     kat += k;
   }
-  Req m{msgs.data(), comp ? nullptr : sigs.data(), KeySource<G1>(), rands.data(), n,
-        seg.data(), nseg, v.data()};
+  Req m{msgs.data(), comp ? nullptr : sigs.data(), KeySource<G1>(), single ? nullptr : rands.data(),
+        n, seg.data(), nseg, v.data()};
   if (r0.src.pts)
     m.src.pts = pts.data();
   else

@@ -9,7 +9,8 @@ The pluggable batching layer in front of the signature hot path:
 * ``SingleVerifier``  -- verifier.rs:171-244 (verifies each triple immediately)
 * ``MultiVerifier``   -- verifier.rs:246-347 (collects triples; ``finish`` runs one
                          random-linear-combination batch on the MI355X engine)
-* ``Triple``          -- verifier.rs:349-429 (``verify_aggregate`` aggregates the keys)
+* ``Triple``          -- verifier.rs:349-429 (``verify_aggregate`` DEFERS the key sum: the key
+                         list is summed on the device by the submission that verifies it)
 * ``VerifierOption``  -- verifier.rs:431-436
 
 Errors follow helper_functions/src/error.rs: ``SignatureInvalid(kind)``; decompression
@@ -49,30 +50,45 @@ class VerifierOption(enum.Enum):
     SkipBlockBaseSignatures = 0
     SkipBlockSyncAggregateSignature = 1
     SkipRandaoVerification = 2
+    BlockImport = 3  # the drop-in's one new option: the engine's block-import class (f3)
 
 
 class Triple:
-    """(message: H256, signature_bytes: SignatureBytes, public_key: PublicKey)."""
+    """(message: H256, signature_bytes: SignatureBytes, public_key: PublicKey), or, after
+    ``verify_aggregate``, the message, signature and the KEY LIST whose sum is the key."""
 
     IS_NULL = False
-    __slots__ = ("message", "signature_bytes", "public_key")
+    __slots__ = ("message", "signature_bytes", "_key", "deferred")
 
     def __init__(self, message: bytes = bytes(32), signature_bytes: bytes = None,
                  public_key: "bls.PublicKey" = None):
         self.message = bytes(message)
         self.signature_bytes = bls.SignatureBytes(signature_bytes if signature_bytes is not None else bytes(96))
-        self.public_key = public_key if public_key is not None else bls.PublicKey.default()
+        self._key = public_key if public_key is not None else bls.PublicKey.default()
+        self.deferred = None  # list of keys once verify_aggregate has run
 
     def verify_aggregate(self, message, signature_bytes, public_keys, signature_kind=None):
-        """verifier.rs:387-405: reduce(AggregatePublicKey::default, aggregate)."""
-        keys = list(public_keys)
-        if keys:
-            pk = bls.PublicKey.aggregate_nonempty(keys)
-        else:
-            pk = bls.PublicKey.default()  # identity of the reduce
+        """verifier.rs:387-405 without the reduce: the keys are kept and summed on the device by
+        the submission that verifies this triple (MultiVerifier.finish /
+        SingleVerifier.extend)."""
         self.message = bytes(message)
         self.signature_bytes = bls.SignatureBytes(bytes(signature_bytes))
-        self.public_key = pk
+        self._key = bls.PublicKey.default()
+        self.deferred = list(public_keys)
+
+    @property
+    def public_key(self) -> "bls.PublicKey":
+        """The set's key: the reference's reduce(AggregatePublicKey::default, aggregate) over a
+        deferred list (one engine sum), or the resolved key."""
+        if self.deferred is None:
+            return self._key
+        if not self.deferred:
+            return bls.PublicKey.default()  # identity of the reduce
+        return bls.PublicKey.aggregate_nonempty(self.deferred)
+
+    def keys(self):
+        """The engine's key operand: the deferred list, or [the key]."""
+        return list(self.deferred) if self.deferred is not None else [self._key]
 
 
 class Verifier:
@@ -134,10 +150,21 @@ class SingleVerifier(Verifier):
             raise SignatureInvalid(signature_kind)
 
     def extend(self, triples, signature_kind):
-        for t in triples:
-            signature = bls.Signature.try_from(t.signature_bytes)
-            if not signature.verify(t.message, t.public_key):
+        """verifier.rs:215-236 as ONE coalesced device submission: every triple's decompression
+        and check together, errors in the reference's order (the first triple whose signature
+        does not decode -> DecompressionFailed, the first that does not verify ->
+        SignatureInvalid)."""
+        triples = list(triples)
+        if not triples:
+            return None
+        outcomes = bls.Signature.verify_batch_compressed(
+            [t.message for t in triples], [t.signature_bytes for t in triples], [t.keys() for t in triples])
+        for status, ok in outcomes:
+            if status != 0:
+                raise bls.DecompressionFailed(status)
+            if not ok:
                 raise SignatureInvalid(signature_kind)
+        return None
 
     def finish(self):
         return None
@@ -169,9 +196,11 @@ class MultiVerifier(Verifier):
         if not self.triples:
             return None
         # decompression (verifier.rs:309-313) and multi_verify in one device submission
+        # key sums of deferred triples (Triple.verify_aggregate) on the device, same submission
         rc = bls.Signature.multi_verify_compressed([t.message for t in self.triples],
                                                    [t.signature_bytes for t in self.triples],
-                                                   [t.public_key for t in self.triples], randoms)
+                                                   [t.keys() for t in self.triples], randoms,
+                                                   0x1 if VerifierOption.BlockImport in self.options else 0)
         if rc not in (0, 5):
             raise bls.DecompressionFailed(rc)
         if rc != 0:

@@ -15,6 +15,10 @@
  *   gbls_verify                 Signature::verify                     bls/src/signature.rs:47-60
  *   gbls_fast_aggregate_verify  Signature::fast_aggregate_verify      bls/src/signature.rs:77-93
  *   gbls_aggregate_verify_batch many independent verify calls         (SingleVerifier::extend, verifier.rs:215-236)
+ *   gbls_verify_batch_compressed  SingleVerifier::extend in ONE submission per call: signature
+ *                               decompression (signature.rs:36-45) fused into the checks, keys
+ *                               single (Triple) or aggregated per check (deferred
+ *                               Triple::verify_aggregate, verifier.rs:387-405)
  *   gbls_multi_verify           Signature::multi_verify               bls/src/signature.rs:95-129
  *                               (reached from MultiVerifier::finish, verifier.rs:301-323)
  *   gbls_multi_verify_segments  several independent multi_verify batches in one submission
@@ -116,12 +120,17 @@ enum {
  * GBLS_INIT_PER_CHECK: batches of independent checks get one Miller product and final
  * exponentiation per check (deterministic, as the reference's fast_aggregate_verify) instead
  * of the grouped form described at gbls_fast_aggregate_verify_batch.
- * The policy flags (GBLS_INIT_NO_COALESCE, GBLS_INIT_PER_CHECK) take effect on every
- * gbls_init call, also on an engine that is already open; the other bits only on the first. */
+ * The policy flags (GBLS_INIT_NO_COALESCE, GBLS_INIT_PER_CHECK) are sticky: a gbls_init call
+ * that names one turns it on, also on an engine that is already open, and no gbls_init call
+ * turns it off (a library's lazy gbls_init(mask, 0) cannot undo a harness's PER_CHECK).  The
+ * other bits apply on the first call only.  gbls_set_policy sets both policies outright
+ * (flags & (GBLS_INIT_NO_COALESCE | GBLS_INIT_PER_CHECK), the rest ignored) and returns the
+ * previous policy bits; it needs no device. */
 #define GBLS_INIT_NO_COALESCE 0x100u
 #define GBLS_INIT_TUNING 0x200u
 #define GBLS_INIT_PER_CHECK 0x400u
 int gbls_init(uint32_t device_mask, uint32_t flags);
+uint32_t gbls_set_policy(uint32_t flags);
 int gbls_last_error(void);
 const char *gbls_version(void);
 int gbls_device_count(void); /* engines (devices x replicas) after gbls_init; 0 before */
@@ -159,10 +168,25 @@ int gbls_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
 int gbls_fast_aggregate_verify(const gbls_p2_affine *sig, const uint8_t *msg, size_t msg_len,
                                const gbls_p1_affine *pks, size_t n);
 /* m independent (sig, msg, pk) checks; messages packed in msg_data with msg_off[m+1];
- * verdicts[i] = GBLS_SUCCESS or GBLS_VERIFY_FAIL. */
+ * verdicts[i] = GBLS_SUCCESS or GBLS_VERIFY_FAIL.
+ * Single checks whose messages are all 32 bytes (signing roots: gbls_verify,
+ * gbls_fast_aggregate_verify and the _batch forms with msg_off[i] == 32 i) are coalesced
+ * across concurrent callers like multi_verify (f3): callers that arrive while the engine is
+ * busy become segments of one submission, each keeping its own verdicts. */
 int gbls_aggregate_verify_batch(const gbls_p2_affine *sigs, const uint8_t *msg_data,
                                 const uint32_t *msg_off, const gbls_p1_affine *pks, size_t m,
                                 int32_t *verdicts);
+/* SingleVerifier::extend (helper_functions/src/verifier.rs:215-236) as ONE coalesced
+ * submission: m checks of 32-byte messages against 96-byte compressed signatures, decompressed
+ * on the device (a8 semantics: sig_status[i] = its BLST_ERROR, the reference's
+ * Signature::try_from) and then verified with Signature::verify semantics (subgroup check,
+ * infinite key rejected).  Keys: pks[i] (pk_off == NULL), or the sum of
+ * pks[pk_off[i] .. pk_off[i+1]) (fast_aggregate_verify; an empty range fails).  verdicts[i] is
+ * GBLS_SUCCESS only when check i decodes and verifies.  Returns GBLS_SUCCESS when every output
+ * was written, else GBLS_VERIFY_FAIL (engine error: gbls_last_error). */
+int gbls_verify_batch_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],
+                                 const gbls_p1_affine *pks, const uint32_t *pk_off, size_t m,
+                                 int32_t *sig_status, int32_t *verdicts);
 /* C3 shape: m fast_aggregate_verify calls, pks of message i = pks[seg_off[i] .. seg_off[i+1]).
  *
  * Grouped verdicts (batches of 2048..65536 independent checks: gbls_aggregate_verify_batch,
@@ -204,8 +228,10 @@ int gbls_multi_verify_indexed(const uint8_t (*msgs)[32], const gbls_p2_affine *s
 /* a2, MultiVerifier::finish (helper_functions/src/verifier.rs:301-323) as ONE submission:
  * the 96-byte compressed signatures are decompressed on the device (a8 semantics, status
  * per signature in sig_status) on the signature-side stream while hash_to_G2 runs, then
- * multi_verify.  Keys: pks (points), or registry indices pk_idx (+ pk_off aggregates) as
- * in gbls_multi_verify_indexed; exactly one of pks / pk_idx.  Returns the first nonzero
+ * multi_verify.  Keys: pks (points) or registry indices pk_idx (exactly one of them), each
+ * either one key per set (pk_off == NULL) or summed per set over [pk_off[i], pk_off[i+1]) --
+ * Triple::verify_aggregate's key sums (verifier.rs:387-405) done inside this one submission
+ * instead of on rayon before it (an empty range fails the batch).  Returns the first nonzero
  * decompression status if any (finish's Err(DecompressionFailed), checked before the
  * verdict), else GBLS_SUCCESS / GBLS_VERIFY_FAIL. */
 int gbls_multi_verify_compressed(const uint8_t (*msgs)[32], const uint8_t (*sigs)[96],

@@ -53,6 +53,7 @@ pub const GBLS_CALL_BLOCK: u32 = 0x1;
 
 extern "C" {
     pub fn gbls_init(device_mask: u32, flags: u32) -> c_int;
+    pub fn gbls_set_policy(flags: u32) -> u32;
     pub fn gbls_last_error() -> c_int;
     pub fn gbls_version() -> *const c_char;
     pub fn gbls_device_count() -> c_int;
@@ -124,6 +125,15 @@ extern "C" {
         msg_off: *const u32,
         pks: *const gbls_p1_affine,
         m: usize,
+        verdicts: *mut i32,
+    ) -> c_int;
+    pub fn gbls_verify_batch_compressed(
+        msgs: *const [u8; 32],
+        sigs: *const [u8; 96],
+        pks: *const gbls_p1_affine,
+        pk_off: *const u32,
+        m: usize,
+        sig_status: *mut i32,
         verdicts: *mut i32,
     ) -> c_int;
     pub fn gbls_fast_aggregate_verify_batch(

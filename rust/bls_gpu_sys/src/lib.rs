@@ -13,9 +13,11 @@
 //!   `Ok(verdict)` only for a real verdict.  The `bls` crate answers `Err` by running the
 //!   original blst body, so a node whose GPU is missing or broken still verifies on the CPU.
 //! * Conversions between blst's raw points (`blst::min_pk::{PublicKey, Signature}`) and the
-//!   engine's point layout go through blst's own uncompressed serialisation, then copy the
-//!   public limb arrays of `blst_fp` / `blst_fp2` field by field: no `transmute`, no reliance
-//!   on the private layout of blst's wrapper types.
+//!   engine's point layout copy the public limb arrays of `blst_fp` / `blst_fp2` field by field:
+//!   blst -> engine through blst's safe `From<&PublicKey> for blst_p1_affine` (and the G2 twin),
+//!   a plain copy of the Montgomery limbs (no serialisation, no curve check: the finish of a
+//!   block converts ~66k keys); engine -> blst through blst's uncompressed decoder, which checks
+//!   the point.  No `transmute`, no reliance on the private layout of blst's wrapper types.
 #![deny(unsafe_op_in_unsafe_fn)]
 
 pub mod ffi;
@@ -124,7 +126,10 @@ static ENGINE: OnceLock<EngineResult<usize>> = OnceLock::new();
 /// Opens the engine once per process on every GPU in `GBLS_DEVICE_MASK` (hex or decimal;
 /// default: every device) and returns the number of engines, or why there is none.  The
 /// result is cached: a node without a usable GPU pays for the probe once and then takes the
-/// CPU path on every call without touching the library again.
+/// CPU path on every call without touching the library again.  `GBLS_PER_CHECK=1` asks for
+/// deterministic per-check verdicts (`GBLS_INIT_PER_CHECK`, e.g. spec-test runs) and
+/// `GBLS_NO_COALESCE=1` turns cross-caller coalescing off; both are sticky in the library, so
+/// no later initialisation clears them (see also [`set_policy`]).
 pub fn engine() -> EngineResult<usize> {
     *ENGINE.get_or_init(|| {
         let mask = std::env::var("GBLS_DEVICE_MASK")
@@ -135,13 +140,28 @@ pub fn engine() -> EngineResult<usize> {
                     .map_or_else(|| v.parse().ok(), |h| u32::from_str_radix(h, 16).ok())
             })
             .unwrap_or(u32::MAX);
+        let on = |name: &str| std::env::var(name).is_ok_and(|v| v.trim() == "1");
+        let mut flags = 0;
+        if on("GBLS_PER_CHECK") {
+            flags |= ffi::GBLS_INIT_PER_CHECK;
+        }
+        if on("GBLS_NO_COALESCE") {
+            flags |= ffi::GBLS_INIT_NO_COALESCE;
+        }
         // SAFETY: plain integers in; the library serialises its own initialisation.
-        let rc = unsafe { ffi::gbls_init(mask, 0) };
+        let rc = unsafe { ffi::gbls_init(mask, flags) };
         status(rc)?;
         // SAFETY: no arguments.
         let n = unsafe { ffi::gbls_device_count() };
         usize::try_from(n).ok().filter(|&n| n > 0).ok_or(EngineError::NoDevice)
     })
+}
+
+/// Sets the engine's policies outright (`GBLS_INIT_PER_CHECK`, `GBLS_INIT_NO_COALESCE`; other
+/// bits ignored) and returns the previous ones.  Needs no device.
+pub fn set_policy(flags: u32) -> u32 {
+    // SAFETY: a plain integer in and out.
+    unsafe { ffi::gbls_set_policy(flags) }
 }
 
 /// `true` when the engine is open (see [`engine`]).
@@ -152,16 +172,11 @@ pub fn available() -> bool {
 
 // ------------------------------------------------------------------ point conversions
 
-/// Engine layout of a blst public key (uncompressed serialisation -> blst affine point ->
-/// limb copy).  A `PublicKey` always holds a point on the curve, so the decode cannot fail.
+/// Engine layout of a blst public key: blst's affine point (its safe `From`), limbs copied.
+/// Both sides hold Montgomery limbs (R = 2^384) with all-zero infinity, so nothing is recomputed.
 #[must_use]
 pub fn p1_of_public_key(key: &RawPublicKey) -> P1 {
-    let bytes = key.serialize();
-    let mut point = blst_p1_affine::default();
-    // SAFETY: `bytes` is the 96-byte uncompressed encoding blst_p1_deserialize reads;
-    // `point` is a valid output location.
-    let rc = unsafe { blst::blst_p1_deserialize(&mut point, bytes.as_ptr()) };
-    debug_assert_eq!(rc, BLST_ERROR::BLST_SUCCESS);
+    let point = blst_p1_affine::from(key);
     P1 { x: point.x.l, y: point.y.l }
 }
 
@@ -178,11 +193,7 @@ pub fn public_key_of_p1(point: &P1) -> Result<RawPublicKey, BLST_ERROR> {
 /// Engine layout of a blst signature (see [`p1_of_public_key`]).
 #[must_use]
 pub fn p2_of_signature(signature: &RawSignature) -> P2 {
-    let bytes = signature.serialize();
-    let mut point = blst_p2_affine::default();
-    // SAFETY: `bytes` is the 192-byte uncompressed encoding blst_p2_deserialize reads.
-    let rc = unsafe { blst::blst_p2_deserialize(&mut point, bytes.as_ptr()) };
-    debug_assert_eq!(rc, BLST_ERROR::BLST_SUCCESS);
+    let point = blst_p2_affine::from(signature);
     P2 { x: [point.x.fp[0].l, point.x.fp[1].l], y: [point.y.fp[0].l, point.y.fp[1].l] }
 }
 
@@ -274,18 +285,39 @@ pub fn multi_verify(messages: &[[u8; 32]], signatures: &[P2], keys: &[P1], scala
     verdict(rc)
 }
 
+/// `key_offsets` describe `n` key ranges over `keys`: n + 1 non-decreasing entries from 0 to
+/// `keys.len()`.
+fn key_ranges_ok(keys: &[P1], key_offsets: &[u32], n: usize) -> bool {
+    key_offsets.len() == n + 1
+        && key_offsets.first() == Some(&0)
+        && key_offsets.windows(2).all(|w| w[0] <= w[1])
+        && usize::try_from(key_offsets[n]).is_ok_and(|last| last == keys.len())
+}
+
+/// Per-set outcome of a compressed check: `Err` = the signature's BLST_ERROR (not decoded).
+fn outcome(status: i32, verdict: i32) -> Result<bool, BLST_ERROR> {
+    if status == ffi::GBLS_SUCCESS {
+        Ok(verdict == ffi::GBLS_SUCCESS)
+    } else {
+        Err(blst_error(status))
+    }
+}
+
 /// a2: `MultiVerifier::finish` as one submission (96-byte signatures decompressed on the
+/// device; set i's key = the sum of `keys[key_offsets[i] .. key_offsets[i + 1]]`, formed on the
 /// device).  `Ok(Err(e))`: the first signature that does not decode, with its BLST_ERROR
 /// (finish's `DecompressionFailed`); `Ok(Ok(v))`: the verdict.
 pub fn multi_verify_compressed(
     messages: &[[u8; 32]],
     signatures: &[[u8; 96]],
     keys: &[P1],
+    key_offsets: &[u32],
     scalars: &[u64],
     class: CallClass,
 ) -> EngineResult<Result<bool, BLST_ERROR>> {
     let n = messages.len();
-    if n == 0 || signatures.len() != n || keys.len() != n || scalars.len() != n || scalars.contains(&0) {
+    if n == 0 || signatures.len() != n || scalars.len() != n || scalars.contains(&0) || !key_ranges_ok(keys, key_offsets, n)
+    {
         return Err(EngineError::Argument);
     }
     let mut statuses = vec![ffi::GBLS_BAD_ENCODING; n];
@@ -293,14 +325,15 @@ pub fn multi_verify_compressed(
         CallClass::Normal => 0,
         CallClass::BlockImport => ffi::GBLS_CALL_BLOCK,
     };
-    // SAFETY: live slices of n elements each (keys as points: no index arrays).
+    // SAFETY: live slices of n elements each, `keys` of key_offsets[n] points and
+    // `key_offsets` of n + 1 entries (checked above; no index arrays).
     let rc = unsafe {
         ffi::gbls_multi_verify_compressed_ex(
             messages.as_ptr(),
             signatures.as_ptr(),
             keys.as_ptr(),
             ptr::null(),
-            ptr::null(),
+            key_offsets.as_ptr(),
             scalars.as_ptr(),
             n,
             statuses.as_mut_ptr(),
@@ -315,6 +348,42 @@ pub fn multi_verify_compressed(
         ffi::GBLS_VERIFY_FAIL => Ok(false),
         decode => Err(blst_error(decode)),
     })
+}
+
+/// a6/a7 for `SingleVerifier::extend`: independent checks of 32-byte messages against 96-byte
+/// signatures (decompressed on the device) and key sums `keys[key_offsets[i] ..
+/// key_offsets[i + 1]]`, in one coalesced submission.  Per set: `Err(e)` = the signature does not
+/// decode (its BLST_ERROR), else whether it verifies.
+pub fn verify_batch_compressed(
+    messages: &[[u8; 32]],
+    signatures: &[[u8; 96]],
+    keys: &[P1],
+    key_offsets: &[u32],
+) -> EngineResult<Vec<Result<bool, BLST_ERROR>>> {
+    let n = messages.len();
+    if signatures.len() != n || !key_ranges_ok(keys, key_offsets, n) {
+        return Err(EngineError::Argument);
+    }
+    if n == 0 {
+        return Ok(Vec::new());
+    }
+    let mut statuses = vec![ffi::GBLS_BAD_ENCODING; n];
+    let mut verdicts = vec![ffi::GBLS_VERIFY_FAIL; n];
+    // SAFETY: live slices of n elements each, `keys` of key_offsets[n] points and `key_offsets`
+    // of n + 1 entries (checked above); n status and n verdict slots.
+    let rc = unsafe {
+        ffi::gbls_verify_batch_compressed(
+            messages.as_ptr(),
+            signatures.as_ptr(),
+            keys.as_ptr(),
+            key_offsets.as_ptr(),
+            n,
+            statuses.as_mut_ptr(),
+            verdicts.as_mut_ptr(),
+        )
+    };
+    status(rc)?;
+    Ok(statuses.into_iter().zip(verdicts).map(|(s, v)| outcome(s, v)).collect())
 }
 
 /// f2: per-set verdicts of a batch (`true` = the set verifies on its own).

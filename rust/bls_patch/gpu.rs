@@ -57,7 +57,9 @@ pub fn signature_point(signature: &Signature) -> P2 {
 }
 
 /// `MultiVerifier::finish` as one engine submission: 96-byte signatures decompressed on the
-/// device, then the random-linear-combination check with the caller's nonzero scalars.
+/// device, set i's key = the sum of `key_points[key_offsets[i] .. key_offsets[i + 1]]` formed on
+/// the device (deferred `Triple::verify_aggregate`), then the random-linear-combination check
+/// with the caller's nonzero scalars.
 /// `None`: no engine verdict (absent engine or engine error) -- the caller runs its blst body.
 /// `Some(Err(e))`: a signature does not decode (`DecompressionFailed(e)`);
 /// `Some(Ok(v))`: the verdict.
@@ -65,15 +67,37 @@ pub fn signature_point(signature: &Signature) -> P2 {
 pub fn multi_verify_compressed(
     messages: &[[u8; 32]],
     signature_bytes: &[[u8; 96]],
-    public_keys: &[P1],
+    key_points: &[P1],
+    key_offsets: &[u32],
     scalars: &[u64],
     class: CallClass,
 ) -> Option<Result<bool, blst::BLST_ERROR>> {
+    counted(|| {
+        bls_gpu_sys::multi_verify_compressed(messages, signature_bytes, key_points, key_offsets, scalars, class)
+    })
+}
+
+/// `SingleVerifier::extend` as one engine submission (coalesced with concurrent callers):
+/// per set, `Err(e)` when its signature does not decode, else whether it verifies against the
+/// sum of its keys.  `None`: no engine verdict -- the caller runs its blst body.
+#[must_use]
+pub fn verify_batch_compressed(
+    messages: &[[u8; 32]],
+    signature_bytes: &[[u8; 96]],
+    key_points: &[P1],
+    key_offsets: &[u32],
+) -> Option<Vec<Result<bool, blst::BLST_ERROR>>> {
+    counted(|| bls_gpu_sys::verify_batch_compressed(messages, signature_bytes, key_points, key_offsets))
+}
+
+/// The engine call's value, or `None` (counted as a CPU fallback) when the engine is absent or
+/// reports an error.
+fn counted<T>(call: impl FnOnce() -> Result<T, EngineError>) -> Option<T> {
     if !available() {
         CPU_FALLBACKS.fetch_add(1, Ordering::Relaxed);
         return None;
     }
-    let result = bls_gpu_sys::multi_verify_compressed(messages, signature_bytes, public_keys, scalars, class);
+    let result = call();
     if result.is_err() {
         CPU_FALLBACKS.fetch_add(1, Ordering::Relaxed);
     }

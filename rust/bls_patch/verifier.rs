@@ -1,0 +1,224 @@
+// Replacement bodies for helper_functions/src/verifier.rs (the Verifier trait, NullVerifier and the
+// options enum stay as they are).  No unsafe code (helper_functions keeps the workspace's
+// `unsafe_code = 'forbid'`).
+//
+// What changes, and why:
+//
+// * `Triple` DEFERS key aggregation.  The reference reduces an attestation's keys on rayon as
+//   soon as the triple is built (`Triple::verify_aggregate`, verifier.rs:387-405:
+//   `par_bridge().reduce(AggregatePublicKey::default, AggregatePublicKey::aggregate)`, one blst
+//   addition plus a field inversion per key).  Here the triple keeps its key list and
+//   `MultiVerifier::finish` hands every list to the engine with per-set offsets
+//   (`gbls_multi_verify_compressed_ex`, points + pk_off): the sums are formed on the device
+//   inside the same submission as decompression, hash_to_G2 and the batch check.  Nothing on
+//   this path calls `AggregatePublicKey::aggregate`; the block path builds its attestation
+//   triples with `Triple::verify_aggregate` directly (transition_functions/src/deneb/
+//   state_transition.rs:161, p2p/src/attestation_verifier.rs:442), so deferring in `Triple`
+//   covers it as well as `MultiVerifier::verify_aggregate`.
+// * `SingleVerifier::extend` verifies all its triples in ONE engine submission
+//   (`gbls_verify_batch_compressed`): decompression and verification together, coalesced with
+//   concurrent callers, instead of a decompression call and a verify call per triple.  Errors
+//   come out in the reference's order: the first triple that fails to decode gives
+//   `DecompressionFailed`, the first that fails to verify `SignatureInvalid(kind)`.
+// * `MultiVerifier::finish` is one submission (verifier.rs:301-323); block import asks for the
+//   engine's block-import priority class through one new option, added to the enum at
+//   verifier.rs:432-436:
+//
+//       pub enum VerifierOption { SkipBlockBaseSignatures, SkipBlockSyncAggregateSignature,
+//                                 SkipRandaoVerification, BlockImport }
+//
+//   which the block paths pass when they build their verifier
+//   (p2p/src/block_verification_pool.rs:109, fork_choice_control/src/tasks.rs:101).
+//
+// Without an engine verdict (no device, engine error) each body runs the reference's blst code,
+// with the deferred sums formed by blst first (`Triple::public_key`).
+
+/// verifier.rs:349-354, plus the deferred key list of `verify_aggregate`.
+#[derive(Default)]
+pub struct Triple {
+    message: H256,
+    signature_bytes: SignatureBytes,
+    public_key: PublicKey,
+    // Some(keys): the public key is the sum of `keys` (Triple::verify_aggregate), not yet formed
+    deferred: Option<Vec<PublicKey>>,
+}
+
+assert_not_impl_any!(Triple: Copy);
+
+impl Triple {
+    /// The reference's `derive(Constructor)` (verifier.rs:349): one resolved key.
+    #[must_use]
+    pub const fn new(message: H256, signature_bytes: SignatureBytes, public_key: PublicKey) -> Self {
+        Self { message, signature_bytes, public_key, deferred: None }
+    }
+
+    /// The set's key for the blst bodies: the deferred sum formed now (reference reduce, identity
+    /// `AggregatePublicKey::default`), or the resolved key.
+    fn public_key(&self) -> PublicKey {
+        match &self.deferred {
+            Some(keys) => keys.iter().copied().fold(AggregatePublicKey::default(), AggregatePublicKey::aggregate),
+            None => self.public_key,
+        }
+    }
+
+    /// The set's keys in the engine's layout, appended to `points` (one point, or the deferred list).
+    fn push_key_points(&self, points: &mut Vec<bls::gpu::P1>) {
+        match &self.deferred {
+            Some(keys) => points.extend(keys.iter().map(bls::gpu::public_key_point)),
+            None => points.push(bls::gpu::public_key_point(&self.public_key)),
+        }
+    }
+}
+
+/// Engine arguments of a run of triples: 32-byte messages, 96-byte signatures, key points and
+/// per-set key offsets (pk_off[i] .. pk_off[i + 1] are set i's keys).
+fn engine_sets(triples: &[Triple]) -> (Vec<[u8; 32]>, Vec<[u8; 96]>, Vec<bls::gpu::P1>, Vec<u32>) {
+    let messages = triples.iter().map(|triple| triple.message.to_fixed_bytes()).collect_vec();
+    let signature_bytes = triples.iter().map(|triple| triple.signature_bytes.to_fixed_bytes()).collect_vec();
+    let mut points = Vec::with_capacity(triples.len());
+    let mut offsets = Vec::with_capacity(triples.len() + 1);
+    offsets.push(0);
+    for triple in triples {
+        triple.push_key_points(&mut points);
+        // a key count past u32 is an argument the engine rejects: the caller falls back to blst
+        offsets.push(u32::try_from(points.len()).unwrap_or(u32::MAX));
+    }
+    (messages, signature_bytes, points, offsets)
+}
+
+impl Verifier for Triple {
+    const IS_NULL: bool = false;
+
+    #[inline]
+    fn reserve(&mut self, _additional: usize) {
+        unimplemented!("<Triple as Verifier>::reserve is not used anywhere")
+    }
+
+    #[inline]
+    fn verify_singular(
+        &mut self,
+        _message: H256,
+        _signature_bytes: SignatureBytes,
+        _cached_public_key: &CachedPublicKey,
+        _signature_kind: SignatureKind,
+    ) -> Result<()> {
+        unimplemented!("<Triple as Verifier>::verify_singular is not used anywhere")
+    }
+
+    /// verifier.rs:387-405 without the rayon reduce: the keys are kept and summed on the device
+    /// by the submission that verifies the triple.
+    #[inline]
+    fn verify_aggregate<'keys>(
+        &mut self,
+        message: H256,
+        signature_bytes: SignatureBytes,
+        public_keys: impl IntoIterator<IntoIter = impl Iterator<Item = &'keys PublicKey> + Send>,
+        _signature_kind: SignatureKind,
+    ) -> Result<()> {
+        let keys = public_keys.into_iter().copied().collect_vec();
+        *self = Self { message, signature_bytes, public_key: PublicKey::default(), deferred: Some(keys) };
+        Ok(())
+    }
+
+    #[inline]
+    fn extend(&mut self, _triples: impl IntoIterator<Item = Self>, _signature_kind: SignatureKind) -> Result<()> {
+        unimplemented!("<Triple as Verifier>::extend is not used anywhere")
+    }
+
+    #[inline]
+    fn finish(&self) -> Result<()> {
+        unimplemented!("<Triple as Verifier>::finish is not used anywhere")
+    }
+
+    #[inline]
+    fn has_option(&self, _option: VerifierOption) -> bool {
+        false
+    }
+}
+
+// ---------------------------------------------------------------- SingleVerifier::extend
+// (verifier.rs:215-236; verify_singular and verify_aggregate keep the reference bodies: the
+// first calls extend, the second Signature::fast_aggregate_verify, which is one engine call)
+
+#[inline]
+fn extend(&mut self, triples: impl IntoIterator<Item = Triple>, signature_kind: SignatureKind) -> Result<()> {
+    let triples = triples.into_iter().collect_vec();
+    if triples.is_empty() {
+        return Ok(());
+    }
+    let (messages, signature_bytes, points, offsets) = engine_sets(&triples);
+    match bls::gpu::verify_batch_compressed(&messages, &signature_bytes, &points, &offsets) {
+        Some(outcomes) => {
+            for outcome in outcomes {
+                // the reference's order per triple: try_from (`?`), then verify
+                let verified = outcome.map_err(bls::Error::DecompressionFailed)?;
+                ensure!(verified, Error::SignatureInvalid(signature_kind));
+            }
+            Ok(())
+        }
+        None => extend_on_cpu(&triples, signature_kind),
+    }
+}
+
+// The reference body (verifier.rs:221-233), a private function next to `impl SingleVerifier`.
+fn extend_on_cpu(triples: &[Triple], signature_kind: SignatureKind) -> Result<()> {
+    for triple in triples {
+        let signature = Signature::try_from(triple.signature_bytes)?;
+        ensure!(signature.verify(triple.message, triple.public_key()), Error::SignatureInvalid(signature_kind));
+    }
+    Ok(())
+}
+
+// ---------------------------------------------------------------- MultiVerifier::finish
+
+#[inline]
+fn finish(&self) -> Result<()> {
+    if self.triples.is_empty() {
+        return Ok(());
+    }
+
+    let (messages, signature_bytes, points, offsets) = engine_sets(&self.triples);
+
+    let mut rng = rand::thread_rng();
+    let randoms = core::iter::repeat_with(|| rng.gen::<NonZeroU64>().get())
+        .take(messages.len())
+        .collect_vec();
+
+    // block verification (transition_functions/src/deneb/state_transition.rs:69-71) is the
+    // latency-critical caller; gossip batches go through the normal class
+    let class = if self.has_option(VerifierOption::BlockImport) {
+        bls::gpu::CallClass::BlockImport
+    } else {
+        bls::gpu::CallClass::Normal
+    };
+
+    match bls::gpu::multi_verify_compressed(&messages, &signature_bytes, &points, &offsets, &randoms, class) {
+        Some(verdict) => {
+            let verdict = verdict.map_err(bls::Error::DecompressionFailed)?;
+            ensure!(verdict, Error::SignatureInvalid(SignatureKind::Multi));
+            Ok(())
+        }
+        None => self.finish_on_cpu(),
+    }
+}
+
+// The reference body (verifier.rs:301-323), added to `impl MultiVerifier` as a private method;
+// deferred sums are formed by blst here (Triple::public_key).
+fn finish_on_cpu(&self) -> Result<()> {
+    let messages = self.triples.iter().map(|triple| triple.message.as_bytes());
+
+    let signatures = self
+        .triples
+        .par_iter()
+        .map(|triple| triple.signature_bytes.try_into())
+        .collect::<Result<Vec<_>, _>>()?;
+
+    let public_keys = self.triples.par_iter().map(Triple::public_key).collect::<Vec<_>>();
+
+    ensure!(
+        Signature::multi_verify(messages, signatures.iter(), public_keys.iter()),
+        Error::SignatureInvalid(SignatureKind::Multi),
+    );
+
+    Ok(())
+}

@@ -1,0 +1,88 @@
+"""Subprocess of tests/test_gpu_dropin.py (its own engine, so the registry it grows is not the
+one the other GPU tests share): gbls_registry_set with GROWTH while registry-indexed
+verifications are still running on a device stream (VERDICT r04 "next 5").
+
+* 8 indexed multi_verify submissions of 8192 sets each are queued on one torch stream
+  (gbls_multi_verify_indexed_segments_device: asynchronous, reading the registry);
+* registry_set then loads keys far past the table's capacity (the table is reallocated and the
+  old one retired behind those readers on the GPU) and must return while the stream is still
+  busy -- no device-wide synchronisation, no host wait for other callers' work;
+* every queued verdict must be right (the readers kept a valid table), and afterwards sets over
+  the old slots and over the new slice verify (the loaded entries were carried over).
+Also replicas (gbls_init flags & 0xff = 2): the same growth on two engines of the one GPU.
+Prints one JSON line."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from grandine_amd import _lib as G  # noqa: E402
+from grandine_amd import factory as F  # noqa: E402
+
+
+def main():
+    import torch
+    replicas = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    L = G.lib(0, replicas)
+    dev = torch.device("cuda", 0)
+    n_reg, n, k = 4096, 8192, 8
+    sks, comp = F.registry(n_reg, seed=b"async")
+    assert not F.load_registry(comp).any()
+    cap0 = L.gbls_registry_size()
+    idx = [(7 * i) % n_reg for i in range(n)]
+    msgs = F.messages(n, b"async")
+    sigs = F.sign([sks[i] for i in idx], msgs)
+    bad = bytearray(sigs)
+    bad[192 * 100:192 * 101] = sigs[192 * 101:192 * 102]
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_msgs, d_sigs, d_bad = t(msgs), t(sigs), t(bytes(bad))
+    d_idx = torch.tensor(idx, dtype=torch.int32, device=dev)
+    d_r = torch.from_numpy(np.array(F.rands(n, 3), dtype=np.uint64).view(np.int64)).to(dev)
+    verdicts = torch.full((k,), -1, dtype=torch.int32, device=dev)
+    off = G.u32_array([0, n])
+    s = torch.cuda.Stream(dev)
+    # warm-up (workspaces sized), then the timed queue
+    with torch.cuda.stream(s):
+        G.check(L.gbls_multi_verify_indexed_segments_device(
+            d_msgs.data_ptr(), d_sigs.data_ptr(), d_idx.data_ptr(), None, d_r.data_ptr(), n, off, 1,
+            verdicts.data_ptr(), ctypes.c_void_p(s.cuda_stream)), "warm")
+    s.synchronize()
+    verdicts.fill_(-1)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        for j in range(k):
+            G.check(L.gbls_multi_verify_indexed_segments_device(
+                d_msgs.data_ptr(), (d_bad if j % 3 == 1 else d_sigs).data_ptr(), d_idx.data_ptr(), None,
+                d_r.data_ptr(), n, off, 1, verdicts[j:].data_ptr(), ctypes.c_void_p(s.cuda_stream)), "queued")
+    # growth while they run: 64 new keys at index 400000 (the table holds ~5k)
+    new_sks, new_comp = F.registry(64, seed=b"async-new")
+    first = 400_000
+    st = (ctypes.c_int32 * 64)()
+    t0 = time.perf_counter()
+    rc = L.gbls_registry_set(first, G.buf(new_comp), 64, st)
+    t_set = time.perf_counter() - t0
+    busy_after_set = not s.query()
+    s.synchronize()
+    t_all = time.perf_counter() - t0
+    res = {"rc": rc, "statuses": sorted(set(st)), "busy_after_set": busy_after_set,
+           "set_ms": round(1e3 * t_set, 3), "queue_ms": round(1e3 * t_all, 3),
+           "verdicts": verdicts.cpu().tolist(), "size": L.gbls_registry_size(), "cap0": cap0,
+           "replicas": L.gbls_device_count()}
+    # old slots and the new slice both resolve after the growth
+    m2 = F.messages(128, b"async-2")
+    i2 = [(13 * i) % n_reg for i in range(64)] + [first + i for i in range(64)]
+    s2 = F.sign([sks[i] for i in i2[:64]] + new_sks, m2)
+    res["after"] = L.gbls_multi_verify_indexed(m2, s2, G.u32_array(i2), None,
+                                               (ctypes.c_uint64 * 128)(*F.rands(128, 4)), 128)
+    res["gap"] = L.gbls_multi_verify_indexed(m2[:32], s2[:192], G.u32_array([first - 1]), None,
+                                             (ctypes.c_uint64 * 1)(5), 1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

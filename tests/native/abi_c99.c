@@ -27,6 +27,7 @@ int main(void) {
   const char *ver;
 
   CALL("gbls_init", gbls_init(0, 0));
+  CALL("gbls_set_policy", gbls_set_policy(0));
   CALL("gbls_device_count", gbls_device_count());
   ver = gbls_version();
   printf("gbls_version %s\n", ver ? ver : "(null)");
@@ -47,6 +48,9 @@ int main(void) {
   CALL("gbls_fast_aggregate_verify", gbls_fast_aggregate_verify(p2, msg, 32, p1, 1));
   CALL("gbls_aggregate_verify_batch", gbls_aggregate_verify_batch(p2, msg, moff, p1, 1, v));
   printf("verdict %d\n", v[0]);
+  CALL("gbls_verify_batch_compressed",
+       gbls_verify_batch_compressed((const uint8_t(*)[32])m32, (const uint8_t(*)[96])s96, p1, NULL, 1,
+                                    st, v));
   CALL("gbls_fast_aggregate_verify_batch",
        gbls_fast_aggregate_verify_batch(p2, msg, moff, p1, off2, 1, v));
   CALL("gbls_fast_aggregate_verify_indexed",
