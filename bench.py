@@ -68,14 +68,16 @@ W_FPMUL = {
     "k_ml_reduce": 0,           # per pair: counted in k_ml_group (the wave levels fold <= 1/G of it)
     "k_ml_horner": 6030,        # per segment: 67 Fp12 squarings + 67 products
     "k_final_verdict": 13357,   # per segment: final exponentiation
-    "k_g1_aggregate_idx": 11,   # per aggregated key: one mixed G1 addition
+    "k_pk_resolve": 11,   # per aggregated key: one mixed G1 addition
 }
 W_PAIR = W_FPMUL["k_lines"] + 884 + 1836  # lines + round-1 leaf + tree (frozen)      # 4228
 W_SEGMENT = W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"] + W_PAIR          # 23615
 W_SET = (W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"] + W_FPMUL["k_mv_g1mul"]
          + W_FPMUL["k_mv_g2mul"] + W_PAIR)                                            # 11815
+DTYPE = ("u32 (exact 381-bit Montgomery: 12 x 32-bit limbs; 14 x 28-bit limbs in the Miller "
+         "products and the square-root exponentiations)")
 W_G2_CHECK = 1251  # sigma subgroup check (fast_aggregate_verify)
-W_C3_MESSAGE = (511 * W_FPMUL["k_g1_aggregate_idx"] + W_G2_CHECK + W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"]
+W_C3_MESSAGE = (511 * W_FPMUL["k_pk_resolve"] + W_G2_CHECK + W_FPMUL["k_h2c_map"] + W_FPMUL["k_h2c_clear"]
                 + 2 * W_PAIR + W_FPMUL["k_ml_horner"] + W_FPMUL["k_final_verdict"])            # 39579
 assert W_C3_MESSAGE == 39579, W_C3_MESSAGE  # BASELINE.md 4, frozen
 
@@ -327,10 +329,10 @@ def main():
 
         leg.stage_units = lambda s: {"k_ml_group": n + nb, "k_ml_reduce": n + nb, "k_lines_S": nb,
                                      "k_ml_horner": nb, "k_final_verdict": nb,
-                                     "k_g1_aggregate_idx": getattr(leg, "pks_per_step", n)}.get(s, n)
+                                     "k_pk_resolve": getattr(leg, "pks_per_step", n)}.get(s, n)
         # whole step, frozen W: sets + per-batch pair/Horner/final exp + key aggregation
         leg.path_fpmul = lambda: (n * W_SET + nb * W_SEGMENT
-                                  + (getattr(leg, "pks_per_step", n) - n) * W_FPMUL["k_g1_aggregate_idx"])
+                                  + (getattr(leg, "pks_per_step", n) - n) * W_FPMUL["k_pk_resolve"])
     # ------------------------------------------------------------------ C3
     elif cfg == "C3":
         m = args.sets or 10_000
@@ -376,7 +378,7 @@ def main():
             segs, g1muls = (m + GROUP - 1) // GROUP + redo, 2 * m
         else:
             redo, segs, g1muls = 0, m, 0
-        leg.stage_units = lambda s: {"k_g1_aggregate_idx": m * k, "k_lines_S": m,
+        leg.stage_units = lambda s: {"k_pk_resolve": m * k, "k_lines_S": m,
                                      "k_ml_group": 2 * m + 2 * redo, "k_ml_reduce": 2 * m + 2 * redo,
                                      "k_ml_horner": segs, "k_final_verdict": segs,
                                      "k_mv_g1mul": max(g1muls // 2, 1)}.get(s, m)
@@ -507,7 +509,10 @@ def main():
                 "traffic": pmc_traffic(dom, cfg == "C2" and args.sets in (0, 4096) and args.batches == 16
                                        and args.inflight == 2),
                 "avg_launch_ms": round(tot_ms / ncalls, 4),
-                "path": {"fpmul_per_step": leg.path_fpmul(),
+                "path": {"work": "W-normalised: BASELINE.md 4's frozen blst-algorithm Fp products per unit "
+                                 "(the engine may execute fewer, e.g. C3's grouped form)",
+                         "fpmul_per_step": leg.path_fpmul(),
+                         "stage_formula_fpmul_per_step": sum(leg.stage_units(k) * W_FPMUL.get(k, 0) for k in stages),
                          "achieved": round(leg.path_fpmul() * MAD_PER_FPMUL * args.steps / dt / 1e12, 4),
                          "frac": round(leg.path_fpmul() * MAD_PER_FPMUL * args.steps / dt / peak, 5)
                          if peak else None},
@@ -524,7 +529,7 @@ def main():
         line = {"metric": leg.metric, "value": round(value, 1),
                 "unit": leg.unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-                "scaling": leg.scaling, "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
+                "scaling": leg.scaling, "vs_baseline": None, "dtype": DTYPE,
                 "data": "synthetic (seeded keys, messages and scalars; signed on device)",
                 "config": {"workload": leg.workload, "config": cfg, "units_per_gpu_per_step": leg.units,
                            "batches_per_step": getattr(leg, "segments", 1), "streams_in_flight": D,
@@ -713,10 +718,31 @@ def bench_c1(args, L, G, F, np):
     for x in ths:
         x.join()
     assert not errs
+    # gossip latency while blocks are imported back to back (sync / backfill): every normal call
+    # that arrives during a block call is held up to 4 ms (measure the hold's cost)
+    stop2 = threading.Event()
+
+    def blocks():
+        while not stop2.is_set():
+            if finish_flags(G.CALL_BLOCK) != G.SUCCESS:
+                errs.append(1)
+
+    bt = threading.Thread(target=blocks)
+    bt.start()
+    time.sleep(0.02)
+    glat_b = []
+    for _ in range(args.steps):
+        t = time.perf_counter()
+        assert L.gbls_multi_verify(gm, gs, gp, r64, 64) == G.SUCCESS
+        glat_b.append(time.perf_counter() - t)
+    stop2.set()
+    bt.join()
+    assert not errs
+    glat_b.sort()
     line = {"metric": "MultiVerifier::finish latency, mainnet-shaped block (C1)", "value": round(lat[len(lat) // 2] * 1e3, 3),
             "unit": "ms (p50)", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(sum(lat) / len(lat) * 1e3, 3), "higher_is_better": False, "scaling": "n/a",
-            "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32 limbs)",
+            "vs_baseline": None, "dtype": DTYPE,
             "data": "synthetic (seeded registry, committees and messages)",
             "config": {"workload": "C1: %d sets (%d keys aggregated from the registry), 96-byte signatures "
                                    "decompressed on the device inside the verify submission, host pointers, PCIe "
@@ -739,6 +765,10 @@ def bench_c1(args, L, G, F, np):
                 "no_priority_p50_ms": round(lat_noprio[len(lat_noprio) // 2] * 1e3, 3),
                 "no_priority_p99_ms": round(lat_noprio[min(len(lat_noprio) - 1, int(len(lat_noprio) * 0.99))] * 1e3, 3),
                 "load": "16 threads x 64-set gbls_multi_verify in a loop"},
+            "gossip64_under_back_to_back_blocks": {
+                "p50_ms": round(glat_b[len(glat_b) // 2] * 1e3, 3),
+                "p99_ms": round(glat_b[min(len(glat_b) - 1, int(len(glat_b) * 0.99))] * 1e3, 3),
+                "load": "one thread importing the C1 block (GBLS_CALL_BLOCK) back to back"},
             "roofline": None, "cpu_baseline": None}
     print(json.dumps(line), flush=True)
 

@@ -78,6 +78,118 @@ HD void g2_psi2_28(g2j28 &r, const g2j28 &p) {
   r.z = p.z;
 }
 
+// a / 2 mod p (a normalized, < 1.03 p): (a + (a odd ? p : 0)) / 2, normalized, < 1.02 p
+HD void half(fe &r, const fe &a) {
+  constexpr uint32_t P[14] = {GBLS_R28_P};
+  const uint32_t odd = a.l[0] & 1u;
+  fe s;
+#pragma unroll
+  for (int i = 0; i < 14; i++) s.l[i] = a.l[i] + (odd ? P[i] : 0u);
+  norm(s);
+#pragma unroll
+  for (int i = 0; i < 13; i++) r.l[i] = (s.l[i] >> 1) | ((s.l[i + 1] & 1u) << 27);
+  r.l[13] = s.l[13] >> 1;
+}
+HD void fe2_half(fe2 &r, const fe2 &a) {
+  half(r.c0, a.c0);
+  half(r.c1, a.c1);
+}
+// 3 b' a = 12 (1 + u) a
+HD void fe2_mul_3b(fe2 &r, const fe2 &a) {
+  fe2 t, s;
+  fe2_mul_xi_r(t, a);
+  fe2_add_r(s, t, t);
+  fe2_add_r(s, s, t);
+  fe2_add_r(s, s, s);
+  fe2_add_r(r, s, s);
+}
+HD void fe2_mul3(fe2 &r, const fe2 &a) {
+  fe2 t;
+  fe2_add_r(t, a, a);
+  fe2_add_r(r, t, a);
+}
+
+// ---------------------------------------------------------------- Miller line steps (k_lines)
+// The lane regime's line steps (k_lines.hip lane_line_dbl / lane_line_add_aff, i.e.
+// bls_pairing.h line_dbl / line_add_aff reordered so each coefficient is handed to `put` as soon
+// as it is known) on a homogeneous point T over r28::fe2: the same operations on the same
+// operands, so the same field values.  put(c, v) receives L0 (c = 0), L2 (c = 2), L3 (c = 4).
+struct g2h28 {
+  fe2 x, y, z;
+};
+template <class Put>
+HD void line_dbl28(g2h28 &T, Put &&put) {
+  fe2 A, B, E, H, t;
+  fe2_sqr(B, T.y);       // Y^2
+  fe2_sqr(t, T.z);       // C = Z^2
+  fe2_mul_3b(E, t);      // 3b'Z^2
+  fe2_add_r(H, T.y, T.z);
+  fe2_sqr(H, H);
+  fe2_sub_r(H, H, B);
+  fe2_sub_r(H, H, t);    // 2YZ                      (C dead)
+  fe2_mul(A, T.x, T.y);
+  fe2_half(A, A);        // XY/2                     (Y dead)
+  f_neg(t, H);
+  put(4, t);             // L3 = -2YZ
+  fe2_sub_r(t, E, B);
+  put(0, t);             // L0 = 3b'Z^2 - Y^2
+  fe2_sqr(t, T.x);
+  fe2_mul3(t, t);
+  put(2, t);             // L2 = 3X^2                (X dead)
+  fe2 F;
+  fe2_add_r(F, E, E);
+  fe2_add_r(F, F, E);    // 3E
+  fe2_sub_r(t, B, F);
+  fe2_mul(T.x, A, t);    // X3 = A (B - F)
+  fe2_mul(T.z, B, H);    // Z3 = B H
+  fe2_add_r(t, B, F);
+  fe2_half(t, t);
+  fe2_sqr(t, t);         // G^2
+  fe2_sqr(E, E);
+  fe2_mul3(E, E);        // 3E^2
+  fe2_sub_r(T.y, t, E);  // Y3 = G^2 - 3E^2
+}
+// T + Q for an affine Q = (qx, qy): theta = Y1 - y2 Z1, lambda = X1 - x2 Z1
+template <class Put>
+HD void line_add28(g2h28 &T, const fe2 &qx, const fe2 &qy, Put &&put) {
+  fe2 th, la, t, u;
+  fe2_mul(t, qy, T.z);
+  fe2_sub_r(th, T.y, t);
+  fe2_mul(t, qx, T.z);
+  fe2_sub_r(la, T.x, t);
+  fe2_mul(u, th, qx);
+  fe2_mul(t, la, qy);
+  fe2_sub_r(u, u, t);
+  put(0, u);             // L0 = theta x2 - lambda y2
+  f_neg(u, th);
+  put(2, u);             // L2 = -theta
+  put(4, la);            // L3 = lambda
+  fe2 vv, vvv, R, A;
+  fe2_sqr(u, th);        // uu
+  fe2_sqr(vv, la);
+  fe2_mul(vvv, vv, la);
+  f_neg(vvv, vvv);       // v^3 = -lambda^3
+  fe2_mul(R, vv, T.x);
+  fe2_mul(A, u, T.z);
+  fe2_sub_r(A, A, vvv);
+  fe2_sub_r(A, A, R);
+  fe2_sub_r(A, A, R);
+  fe2_mul(T.x, la, A);
+  f_neg(T.x, T.x);       // X3 = v A
+  fe2_sub_r(t, R, A);
+  fe2_mul(t, th, t);
+  f_neg(t, t);           // u (R - A)
+  fe2_mul(R, vvv, T.y);
+  fe2_sub_r(T.y, t, R);
+  fe2_mul(T.z, vvv, T.z);
+}
+
+// a radix-2^28 value stored in an engine-layout slot without conversion: the 392-bit limb
+// vector of a normalized value < 2^384 repacked into 12 words (no product: the value times
+// 2^392 mod p, which an engine-form reader sees as the value times 2^8)
+HD void store12(fp &dst, const fe &a) { repack_out(dst, a); }
+HD void load12(fe &r, const fp &src) { repack_in(r, src); }
+
 // h_eff P, the sequence of clear_cofactor_g2 (bls_hash.h, Budroni-Pintore): host tests of
 // the layer's G2 formulas (tests/native/host_harness.cpp)
 HD void clear_cofactor28(g2j28 &r, const g2j28 &p) {

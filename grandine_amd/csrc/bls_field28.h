@@ -110,6 +110,28 @@ HD void mul2(fe &r, const fe &a, const fe &b, const fe &c, const fe &d) {
 #endif
 }
 
+// x0 y0 + ... + x5 y5 in one reduction (one operand of each pair normalized, the other with
+// limbs < 2^29; values < 34 p^2 in all: output < 1.02 p)
+HD void mul6(fe &r, const fe &x0, const fe &y0, const fe &x1, const fe &y1, const fe &x2, const fe &y2,
+             const fe &x3, const fe &y3, const fe &x4, const fe &y4, const fe &x5, const fe &y5) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mul6_dev(r, x0, y0, x1, y1, x2, y2, x3, y3, x4, y4, x5, y5);
+#else
+  const fe *x[6] = {&x0, &x1, &x2, &x3, &x4, &x5}, *y[6] = {&y0, &y1, &y2, &y3, &y4, &y5};
+  mul_n<6>(r, x, y);
+#endif
+}
+
+HD void mul4(fe &r, const fe &x0, const fe &y0, const fe &x1, const fe &y1, const fe &x2, const fe &y2,
+             const fe &x3, const fe &y3) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mul4_dev(r, x0, y0, x1, y1, x2, y2, x3, y3);
+#else
+  const fe *x[4] = {&x0, &x1, &x2, &x3}, *y[4] = {&y0, &y1, &y2, &y3};
+  mul_n<4>(r, x, y);
+#endif
+}
+
 HD void norm(fe &a) {
 #pragma unroll
   for (int i = 0; i < 13; i++) {
@@ -456,6 +478,124 @@ HD void fe12_mul_034_st(fe12 &r, const fe12 &a, const sp &s, uint32_t *st, uint3
   fe2_add_r(r.c0.c1, t0.c1, t1.c0);
   fe2_add_r(r.c0.c2, t0.c2, t1.c1);
 }
+// f <- f (a0 + a2 w^2 + a3 w^3) with ONE reduction per output Fp coordinate (lazy reduction):
+// in the w basis f = sum f_i w^i (f0 = c0.c0, f1 = c1.c0, f2 = c0.c1, f3 = c1.c1, f4 = c0.c2,
+// f5 = c1.c2; w^6 = xi) the product's coefficients are
+//   r0 = f0 a0 + f4 b2 + f3 b3      r3 = f3 a0 + f1 a2 + f0 a3
+//   r1 = f1 a0 + f5 b2 + f4 b3      r4 = f4 a0 + f2 a2 + f1 a3
+//   r2 = f2 a0 + f0 a2 + f5 b3      r5 = f5 a0 + f3 a2 + f2 a3       (b = xi a)
+// so each Fp coordinate is six Fp products, summed in one product-scanning pass and reduced
+// once (mul6): 72 products + 12 reductions against the Karatsuba form's 52 products + 26
+// reductions and ~60 Fp additions/subtractions (the r04 kernel), and no Fp12 temporaries:
+// the outputs are written in place in the order r3 r4 r5 r2 r0 r1, which frees each input
+// after its last use, with at most three outputs parked.  The minus signs of Re(x y) =
+// x0 y0 - x1 y1 ride in negated line operands (4p - y1, limbs < 2^29).  Line coefficients
+// normalized and < 1.1 p; f normalized and < 1.1 p; outputs normalized and < 1.02 p.
+HD void fe2_mul3_acc(fe2 &r, const fe2 &x, const fe2 &u, const fe &nu1, const fe2 &y, const fe2 &v,
+                     const fe &nv1, const fe2 &z, const fe2 &t, const fe &nt1) {
+  // r = x u + y v + z t (Fp2), nu1 = 4p - u.c1 etc.
+  mul6(r.c0, x.c0, u.c0, x.c1, nu1, y.c0, v.c0, y.c1, nv1, z.c0, t.c0, z.c1, nt1);
+  mul6(r.c1, x.c0, u.c1, x.c1, u.c0, y.c0, v.c1, y.c1, v.c0, z.c0, t.c1, z.c1, t.c0);
+}
+HD void fe12_mul_034_lazy(fe12 &f, const sp &s) {
+  fe2 &f0 = f.c0.c0, &f1 = f.c1.c0, &f2 = f.c0.c1, &f3 = f.c1.c1, &f4 = f.c0.c2, &f5 = f.c1.c2;
+  fe n0, n2, n3;
+  neg_lazy(n0, s.a0.c1);
+  neg_lazy(n2, s.a2.c1);
+  neg_lazy(n3, s.a3.c1);
+  fe2 r3, r4, r5, x;
+  fe2_mul3_acc(r3, f3, s.a0, n0, f1, s.a2, n2, f0, s.a3, n3);
+  fe2_mul3_acc(r4, f4, s.a0, n0, f2, s.a2, n2, f1, s.a3, n3);
+  fe2_mul3_acc(r5, f5, s.a0, n0, f3, s.a2, n2, f2, s.a3, n3);
+  fe2 b3, b2;
+  sub(b3.c0, s.a3.c0, s.a3.c1);  // xi a3 (< 5.1 p, normalized)
+  add(b3.c1, s.a3.c0, s.a3.c1);
+  neg_lazy(n3, b3.c1);
+  fe2_mul3_acc(x, f2, s.a0, n0, f0, s.a2, n2, f5, b3, n3);
+  f2 = x;  // r2 (f2's last use)
+  sub(b2.c0, s.a2.c0, s.a2.c1);  // xi a2
+  add(b2.c1, s.a2.c0, s.a2.c1);
+  neg_lazy(n2, b2.c1);
+  fe2_mul3_acc(x, f0, s.a0, n0, f4, b2, n2, f3, b3, n3);
+  f0 = x;  // r0 (last use of f0 and f3)
+  f3 = r3;
+  fe2_mul3_acc(x, f1, s.a0, n0, f5, b2, n2, f4, b3, n3);
+  f1 = x;  // r1 (last use of f1, f4, f5)
+  f4 = r4;
+  f5 = r5;
+}
+
+// fe12_mul_034_lazy with the three parked outputs (r3, r4, r5: 84 words) in a per-lane stash
+// (LDS in k_ml_group28, word i of the lane at st[i * stride]): 84 fewer live registers
+HD void fe2_stash(uint32_t *st, uint32_t stride, const fe2 &a) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(&a);
+#pragma unroll
+  for (int i = 0; i < 28; i++) st[i * stride] = w[i];
+}
+HD void fe2_unstash(fe2 &a, const uint32_t *st, uint32_t stride) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(&a);
+#pragma unroll
+  for (int i = 0; i < 28; i++) w[i] = st[i * stride];
+}
+HD void fe12_mul_034_lazy_st(fe12 &f, const sp &s, uint32_t *st, uint32_t stride) {
+  fe2 &f0 = f.c0.c0, &f1 = f.c1.c0, &f2 = f.c0.c1, &f3 = f.c1.c1, &f4 = f.c0.c2, &f5 = f.c1.c2;
+  fe n0, n2, n3;
+  neg_lazy(n0, s.a0.c1);
+  neg_lazy(n2, s.a2.c1);
+  neg_lazy(n3, s.a3.c1);
+  fe2 x;
+  fe2_mul3_acc(x, f3, s.a0, n0, f1, s.a2, n2, f0, s.a3, n3);
+  fe2_stash(st, stride, x);  // r3
+  fe2_mul3_acc(x, f4, s.a0, n0, f2, s.a2, n2, f1, s.a3, n3);
+  fe2_stash(st + 28 * stride, stride, x);  // r4
+  fe2_mul3_acc(x, f5, s.a0, n0, f3, s.a2, n2, f2, s.a3, n3);
+  fe2_stash(st + 56 * stride, stride, x);  // r5
+  fe2 b3, b2;
+  sub(b3.c0, s.a3.c0, s.a3.c1);  // xi a3
+  add(b3.c1, s.a3.c0, s.a3.c1);
+  neg_lazy(n3, b3.c1);
+  fe2_mul3_acc(x, f2, s.a0, n0, f0, s.a2, n2, f5, b3, n3);
+  f2 = x;  // r2
+  sub(b2.c0, s.a2.c0, s.a2.c1);  // xi a2
+  add(b2.c1, s.a2.c0, s.a2.c1);
+  neg_lazy(n2, b2.c1);
+  fe2_mul3_acc(x, f0, s.a0, n0, f4, b2, n2, f3, b3, n3);
+  f0 = x;  // r0
+  fe2_unstash(f3, st, stride);
+  fe2_mul3_acc(x, f1, s.a0, n0, f5, b2, n2, f4, b3, n3);
+  f1 = x;  // r1
+  fe2_unstash(f4, st + 28 * stride, stride);
+  fe2_unstash(f5, st + 56 * stride, stride);
+}
+
+// (a0 + a2 w^2 + a3 w^3)(b0 + b2 w^2 + b3 w^3) with one reduction per output Fp coordinate:
+//   r0 = a0 b0 + a3 (xi b3), r1 = 0, r2 = a0 b2 + a2 b0, r3 = a0 b3 + a3 b0, r4 = a2 b2,
+//   r5 = a2 b3 + a3 b2
+// (four products per coordinate, two for r4).  Inputs normalized, < 1.1 p; outputs < 1.01 p.
+HD void sp_mul_sp_lazy(fe12 &r, const sp &a, const sp &b) {
+  fe n0, n2, n3;
+  neg_lazy(n0, b.a0.c1);
+  neg_lazy(n2, b.a2.c1);
+  neg_lazy(n3, b.a3.c1);
+  // x u + y v (Fp2), nu1 = 4p - u.c1
+  auto mul2_acc = [](fe2 &o, const fe2 &x, const fe2 &u, const fe &nu1, const fe2 &y, const fe2 &v,
+                     const fe &nv1) {
+    mul4(o.c0, x.c0, u.c0, x.c1, nu1, y.c0, v.c0, y.c1, nv1);
+    mul4(o.c1, x.c0, u.c1, x.c1, u.c0, y.c0, v.c1, y.c1, v.c0);
+  };
+  mul2_acc(r.c0.c1, a.a0, b.a2, n2, a.a2, b.a0, n0);                   // r2
+  mul2_acc(r.c1.c1, a.a0, b.a3, n3, a.a3, b.a0, n0);                   // r3
+  mul2_acc(r.c1.c2, a.a2, b.a3, n3, a.a3, b.a2, n2);                   // r5
+  mul2(r.c0.c2.c0, a.a2.c0, b.a2.c0, a.a2.c1, n2);                     // r4
+  mul2(r.c0.c2.c1, a.a2.c0, b.a2.c1, a.a2.c1, b.a2.c0);
+  fe2 x;
+  sub(x.c0, b.a3.c0, b.a3.c1);  // xi b3
+  add(x.c1, b.a3.c0, b.a3.c1);
+  neg_lazy(n3, x.c1);
+  mul2_acc(r.c0.c0, a.a0, b.a0, n0, a.a3, x, n3);                      // r0
+  fe2_zero(r.c1.c0);                                                   // r1
+}
+
 // sparse line from engine-form line coefficients and an engine-form g1s point, with no
 // conversion: the product of two engine-form words over R = 2^392 is the radix-2^28 form of
 // L P times 2^-16, a scalar that the final exponentiation removes (as the g1s scaling does)

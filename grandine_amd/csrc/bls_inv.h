@@ -6,6 +6,13 @@
 // Every input on the verification path is public, so variable time is fine.
 //
 // Same contract as fp_inv: Montgomery form in (a R), Montgomery form out (a^-1 R), 0 -> 0.
+//
+// Attribution: the structure follows the public variable-time safegcd of libsecp256k1
+// (src/modinv32_impl.h, MIT licence: secp256k1_modinv32_var with its divsteps_30_var /
+// update_de_30 / update_fg_30_var decomposition and the ctz(g | (~0 << i)) zero-skipping loop),
+// itself an implementation of D. J. Bernstein and B.-Y. Yang, "Fast constant-time gcd
+// computation and modular inversion" (TCHES 2019).  Re-targeted here to 13 x 30-bit limbs of the
+// BLS12-381 base field and to the engine's Montgomery form; not code of the reference repository.
 #pragma once
 #include "bls_field.h"
 

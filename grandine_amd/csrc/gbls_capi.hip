@@ -44,7 +44,10 @@ static_assert(sizeof(g2a) == sizeof(gbls_p2_affine), "p2 layout");
 static_assert(sizeof(fp12) == sizeof(gbls_fp12), "fp12 layout");
 
 uint32_t gbls::g_row_clear_max = gbls::kRowClearMax;
-uint32_t gbls::g_ml_r28 = 0;
+uint32_t gbls::g_ml_r28 = 1;
+uint32_t gbls::g_msm_k = gbls::kMsmChunk;
+uint32_t gbls::g_ml_xcd = 1;
+uint32_t gbls::g_lane_r28 = 1;
 
 namespace {
 
@@ -93,7 +96,7 @@ enum Stage {
 const char *kStageNames[S_COUNT] = {"k_h2c_field", "k_h2c_map",   "k_h2c_clear", "k_mv_g1mul",
                                     "k_mv_g2mul",  "k_g2sum",      "k_lines",     "k_lines_S",
                                     "k_ml_group",  "k_ml_reduce",  "k_ml_horner", "k_final_verdict",
-                                    "k_g1_aggregate_idx", "k_msm"};
+                                    "k_pk_resolve", "k_msm"};
 
 struct Prof {
   std::mutex mu;
@@ -138,8 +141,8 @@ struct Ctx {
   // verified (created on first use, see Engine::block_reserve)
   hipStream_t own_g = nullptr, side1_g = nullptr, side2_g = nullptr;
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
-             ev_done = nullptr, ev_upl = nullptr, ev_in = nullptr, ev_out = nullptr;
-  bool done_pending = false, upl_pending = false;
+             ev_done = nullptr, ev_in = nullptr, ev_out = nullptr;
+  bool done_pending = false;
   // recorded behind this context's last kernel that read the validator registry (written under
   // the shared registry lock, read by gbls_registry_set under the exclusive one): a grown
   // registry's old table is freed only after every such reader
@@ -150,15 +153,26 @@ struct Ctx {
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
-  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, Sj, gpart, lines, Ts, V0, V1, hparts, tab, part, err, out0,
+  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, Sj, gpart, lines, Ts, V0, V1, V28, hparts, tab, part, err, out0,
       out1, pks, pre, pre2, msm, sigd, sigst, rnd, ng1, gerr, gv, redo, rtab;
   // per-call option of the next pipeline_partials on this lease: compressed signatures
   // (96 B each, device) to decompress on the signature-side stream into `sigs`, with their
   // BLST_ERROR statuses (device) failing their segments (consumed and reset by the pipeline)
   const uint8_t *sig_c = nullptr;
   int32_t *sig_st = nullptr;
-  void *stage = nullptr;
-  size_t stage_cap = 0, stage_used = 0;
+  // Pinned staging for host tables and host inputs: a ring of kStageRing buffers, one per call,
+  // each recycled only once the uploads of the call that used it have landed.  (One buffer made
+  // every call wait on the host for the previous call's uploads, which are queued behind that
+  // call's predecessor on the GPU: a device entry point ran at most ~2 calls ahead of the GPU.)
+  static constexpr int kStageRing = 4;
+  struct Stage {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;  // after this buffer's last upload
+    bool pending = false;
+  } ring[kStageRing];
+  int stage_at = 0;
+  size_t stage_used = 0;
   std::vector<uint32_t> host_tab;  // table assembly, reused across calls
 
   bool init(int dev, bool side2_high, int prio_mode, int klass) {
@@ -183,7 +197,7 @@ struct Ctx {
     HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ev_upl, hipEventDisableTiming));
+    for (Stage &r : ring) HIPCHK(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_reg, hipEventDisableTiming));
     return true;
   }
@@ -219,9 +233,11 @@ struct Ctx {
   bool begin(hipStream_t st) {
     cur = st;
     active = true;
-    if (upl_pending) {
-      HIPCHK(hipEventSynchronize(ev_upl));
-      upl_pending = false;
+    stage_at = (stage_at + 1) % kStageRing;  // this call's staging buffer
+    Stage &r = ring[stage_at];
+    if (r.pending) {  // only when kStageRing calls of this context are still uploading
+      HIPCHK(hipEventSynchronize(r.ev));
+      r.pending = false;
     }
     stage_used = 0;
     if (done_pending) HIPCHK(hipStreamWaitEvent(st, ev_done, 0));
@@ -252,23 +268,24 @@ struct Ctx {
   // bump allocation in the pinned staging buffer (per call); regrowing waits for the
   // uploads of this call that still read it
   void *staging(size_t bytes) {
+    Stage &r = ring[stage_at];
     size_t need = (bytes + 255) & ~(size_t)255;
-    if (stage_used + need > stage_cap) {
-      if (upl_pending) {
-        if (hipEventSynchronize(ev_upl) != hipSuccess) return nullptr;
-        upl_pending = false;
+    if (stage_used + need > r.cap) {
+      if (r.pending) {
+        if (hipEventSynchronize(r.ev) != hipSuccess) return nullptr;
+        r.pending = false;
       }
-      if (need > stage_cap) {
-        if (stage) (void)hipHostFree(stage);
-        stage = nullptr;
-        stage_cap = 0;
+      if (need > r.cap) {
+        if (r.p) (void)hipHostFree(r.p);
+        r.p = nullptr;
+        r.cap = 0;
         size_t want = std::max<size_t>(need * 2, 1 << 20);
-        if (hipHostMalloc(&stage, want, hipHostMallocDefault) != hipSuccess) return nullptr;
-        stage_cap = want;
+        if (hipHostMalloc(&r.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+        r.cap = want;
       }
       stage_used = 0;
     }
-    void *p = static_cast<uint8_t *>(stage) + stage_used;
+    void *p = static_cast<uint8_t *>(r.p) + stage_used;
     stage_used += need;
     return p;
   }
@@ -279,8 +296,8 @@ struct Ctx {
     if (!s) return fail(GBLS_ERR_HIP);
     std::memcpy(s, host, bytes);
     HIPCHK(hipMemcpyAsync(dst.p, s, bytes, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(ev_upl, st));
-    upl_pending = true;
+    HIPCHK(hipEventRecord(ring[stage_at].ev, st));
+    ring[stage_at].pending = true;
     return true;
   }
 };
@@ -400,6 +417,9 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_ROW_CLEAR_MAX"))
       g_row_clear_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_CU_SPLIT")) g.cu_split = std::atoi(e);
+    if (const char *e = std::getenv("GBLS_MSM_K")) g_msm_k = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char *e = std::getenv("GBLS_ML_XCD")) g_ml_xcd = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_LANE_R28")) g_lane_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_CU_SPLIT_MAX"))
       g.cu_split_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LEADERS")) g.leaders = std::max(1, std::atoi(e));
@@ -407,9 +427,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_MERGE_WINDOW_US")) g.merge_window_us = std::atoi(e);
     if (const char *e = std::getenv("GBLS_BLOCK_RESERVE")) g.block_reserve = std::atoi(e);
     if (const char *e = std::getenv("GBLS_BLOCK_HOLD")) g.block_hold = std::atoi(e) != 0;
-#ifdef GBLS_EXPERIMENTS
     if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
-#endif
   }
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
@@ -734,6 +752,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
       !c.ensure(c.gpart, nchunks * (sizeof(g2j) + 4)) || !c.ensure(c.lines, line_words * 4) ||
       !c.ensure(c.V0, ML_EVENTS * mt.v0_n * sizeof(fp12)) ||
       !c.ensure(c.V1, ML_EVENTS * mt.v1_n * sizeof(fp12)) ||
+      (g_ml_r28 && !c.ensure(c.V28, (size_t)ML_EVENTS * 168 * 4 * mt.ngroup)) ||
       !c.ensure(c.hparts, 4 * 64 * sizeof(fp12)))  // the split Horner's parts (<= 64 segments)
     return false;
   if (!c.upload_staged(c.tab, tab.data(), tab.size() * 4, st)) return false;
@@ -839,7 +858,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     }
     StageTimer t(S_ML_LEAF, st);
     launch_ml_group(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T + mt.plist_off,
-                    T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>());
+                    T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>(), c.V28.as<uint32_t>());
   }
   ml_tail(c, st, mt, T, (uint32_t)nms, partials, n <= kSplitHornerMaxSets);
   if (st != caller) {
@@ -910,7 +929,8 @@ bool grouped_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *ms
       !c.ensure(c.part, n * sizeof(fp12)) || !c.ensure(c.err, n * sizeof(int32_t) + 16) ||
       !c.ensure(c.gerr, n * sizeof(int32_t) + 16) || !c.ensure(c.gv, n * sizeof(int32_t) + 16) ||
       !c.ensure(c.redo, (n + 16) * sizeof(uint32_t)) || !c.ensure(c.rtab, 5 * R * sizeof(uint32_t)) ||
-      !c.ensure(c.V0, ML_EVENTS * R * sizeof(fp12)))
+      !c.ensure(c.V0, ML_EVENTS * R * sizeof(fp12)) ||
+      (g_ml_r28 && !c.ensure(c.V28, (size_t)ML_EVENTS * 168 * 4 * R)))
     return false;
   size_t nms = 0;
   if (!pipeline_partials(c, d, msgs, msg_off, sigs, src, nullptr, sig_groupcheck, n, seg_off, n, 1,
@@ -937,7 +957,7 @@ bool grouped_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *ms
     {
       StageTimer t(S_ML_LEAF, st);
       launch_ml_group(st, c.lines.as<uint32_t>(), (uint32_t)(2 * n), c.P.as<g1s>(), plist, grp, (uint32_t)R, 0,
-                      ML_EVENTS, c.V0.as<fp12>());
+                      ML_EVENTS, c.V0.as<fp12>(), c.V28.as<uint32_t>());
     }
     {
       StageTimer t(S_ML_HORNER, st);
@@ -1253,7 +1273,9 @@ bool bisect_host(const uint8_t *msgs, const g2a *sigs, const PkSource &src,
 bool registry_streams(Device &d) {
   if (d.reg_st) return true;
   HIPCHK(hipSetDevice(d.hipdev));
-  HIPCHK(hipStreamCreateWithFlags(&d.reg_st, hipStreamNonBlocking));
+  int least = 0, greatest = 0;  // registry updates are small: they jump the queued normal work
+  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  HIPCHK(hipStreamCreateWithPriority(&d.reg_st, hipStreamNonBlocking, greatest));
   HIPCHK(hipStreamCreateWithFlags(&d.retire_st, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&d.reg_ev, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&d.reg_tmp, hipEventDisableTiming));

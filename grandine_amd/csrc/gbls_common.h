@@ -35,6 +35,10 @@ constexpr uint32_t kW4Max = GBLS_W4_MAX;
 constexpr uint32_t kRowClearMax = 2048;
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
 extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic (GBLS_ML_R28)
+constexpr uint32_t kMsmChunk = 8;        // k_msm_chunk: points summed per lane before the folds
+extern uint32_t g_msm_k;                 // kMsmChunk unless GBLS_MSM_K is set
+extern uint32_t g_ml_xcd;                // k_ml_group: XCD-grouped block order (GBLS_ML_XCD)
+extern uint32_t g_lane_r28;              // lane-regime clearing / lines in radix 2^28 (GBLS_LANE_R28)
 // line-coefficient buffer bound per submission (19.6 KB per pair: 4 GB = 214k pairs,
 // a C5 shard of 131 072 sets unsliced; tiny next to 288 GB of HBM): above it the Miller
 // lines are made in event slices (GBLS_LINE_BUDGET_MB overrides it)
@@ -99,6 +103,7 @@ struct MsmPlan {
   int c, W;             // window bits, windows
   uint32_t nb;          // buckets (nseg * W * 2^(c-1))
   uint32_t max_chunks;  // bound on the chunk count (grid of the chunk kernel)
+  uint32_t K;           // points per chunk
   bool tree;            // per-window bucket trees (c = 13) or per-bucket pairs (c = 5)
   uint32_t extra;       // extra Miller pairs per segment: W (tree) or W * 2^(c-1)
   size_t o_cnt, o_start, o_cur, o_cstart, o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
@@ -132,7 +137,7 @@ bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t f
 // events [e0, e1): lines at event e - e0, products to V0[e * ngroup + g]
 void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
                      const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
-                     int e1, fp12 *V0);
+                     int e1, fp12 *V0, uint32_t *V28);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);
 // lim (device count, optional): only segments s with base + s < *lim run (the others exit)

@@ -35,14 +35,21 @@ __device__ __forceinline__ void gang_clear_cofactor_g2(g2j &r, const g2j &p, int
 
 // stage 3: Q0 + Q1, clear the cofactor (Budroni-Pintore), affine.  4 lanes per message;
 // a quad never straddles the n boundary (the whole quad returns together).
+// P = Q0 + Q1 waits in LDS (72 words per lane) while the chains run: 35 spilled VGPRs (48 B of
+// scratch per lane) down to 3 (12 B, ten scratch instructions in the kernel)
 __global__ void __launch_bounds__(WG) k_h2c_clear(const g2j *Q, uint32_t n, g2a *H) {
   uint32_t t = blockIdx.x * WG + threadIdx.x;
   uint32_t i = t >> 2;
   int q = (int)(t & 3);
   if (i >= n) return;
-  g2j a = Q[2 * i], b = Q[2 * i + 1], h;
-  gang_add(a, a, b, q);
-  gang_clear_cofactor_g2(h, a, q);
+  __shared__ g2j pl[WG];
+  g2j h;
+  {
+    g2j a = Q[2 * i], b = Q[2 * i + 1];
+    gang_add(a, a, b, q);
+    pl[threadIdx.x] = a;
+  }
+  gang_clear_cofactor_g2(h, pl[threadIdx.x], q);
   g2a o;
   jac_to_aff(o, h);
   if (q == 0) H[i] = o;
@@ -149,6 +156,93 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane_b(const g2j *Q, uint32_t 
   H[i] = o;
 }
 
+// The two lane-form chains in radix 2^28 (bls_curve28.h: the engine's Jacobian templates over
+// r28::fe2, one v_mad_u64_u32 per product term), the default since r05 (g_lane_r28).  The chain's
+// base point waits in LDS for its 5 additions (84 words per lane), which keeps both kernels
+// free of scratch; between the chains the message's Q slots hold the radix-2^28 limbs repacked
+// into the engine layout (store12, no conversion product); chain b converts its result to
+// engine form (to_fp) before the affine conversion, so H is bit-identical to the 32-bit path's.
+__device__ __forceinline__ void g2j28_store(g2j &dst, const r28::g2j28 &a) {
+  r28::store12(dst.x.c0, a.x.c0), r28::store12(dst.x.c1, a.x.c1);
+  r28::store12(dst.y.c0, a.y.c0), r28::store12(dst.y.c1, a.y.c1);
+  r28::store12(dst.z.c0, a.z.c0), r28::store12(dst.z.c1, a.z.c1);
+}
+__device__ __forceinline__ void g2j28_load(r28::g2j28 &r, const g2j &src) {
+  r28::load12(r.x.c0, src.x.c0), r28::load12(r.x.c1, src.x.c1);
+  r28::load12(r.y.c0, src.y.c0), r28::load12(r.y.c1, src.y.c1);
+  r28::load12(r.z.c0, src.z.c0), r28::load12(r.z.c1, src.z.c1);
+}
+// h = [|x|] (*pl), the base read from LDS at each of the 5 additions
+__device__ __forceinline__ void mul_by_xabs28(r28::g2j28 &h, const r28::g2j28 *pl) {
+  h = *pl;
+  for (int b = 62; b >= 0; b--) {
+    jac_dbl(h, h);
+    if ((k::X_ABS >> b) & 1) jac_add(h, h, *pl);
+  }
+}
+__global__ void __launch_bounds__(WG) k_h2c_clear_lane_a28(g2j *Q, uint32_t n) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  __shared__ r28::g2j28 pl[WG];
+  r28::g2j28 *pp = pl + threadIdx.x;
+  r28::g2j28 t1;
+  {
+    r28::g2j28 p, q;
+    const g2j e0 = Q[2 * i];
+    r28::g2j_in(p, e0);
+    const g2j e1 = Q[2 * i + 1];
+    r28::g2j_in(q, e1);
+    jac_add(p, p, q);  // P = Q0 + Q1
+    *pp = p;
+  }
+  mul_by_xabs28(t1, pp);
+  jac_neg(t1, t1);  // t1 = [x]P
+  {
+    r28::g2j28 t2;
+    r28::g2_psi28(t2, *pp);
+    jac_add(t2, t2, t1);  // t2 = t1 + psi(P)
+    g2j28_store(Q[2 * i], t2);
+  }
+  jac_neg(t1, t1);  // -t1
+  {
+    r28::g2j28 v;
+    jac_neg(v, *pp);
+    jac_add(t1, t1, v);  // - t1 - P
+    jac_dbl(v, *pp);
+    r28::g2_psi2_28(v, v);
+    jac_add(t1, t1, v);  // + psi^2(2P)
+    r28::g2_psi28(v, *pp);
+    jac_neg(v, v);
+    jac_add(t1, t1, v);  // - psi(P)
+  }
+  g2j28_store(Q[2 * i + 1], t1);
+}
+__global__ void __launch_bounds__(WG) k_h2c_clear_lane_b28(const g2j *Q, uint32_t n, g2a *H) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  __shared__ r28::g2j28 pl[WG];
+  r28::g2j28 *pp = pl + threadIdx.x;
+  r28::g2j28 h;
+  {
+    r28::g2j28 t2;
+    g2j28_load(t2, Q[2 * i]);
+    *pp = t2;
+  }
+  mul_by_xabs28(h, pp);
+  jac_neg(h, h);  // [x] t2
+  {
+    r28::g2j28 T;
+    g2j28_load(T, Q[2 * i + 1]);
+    *pp = T;
+    jac_add(h, h, *pp);
+  }
+  g2j e;
+  r28::g2j_out(e, h);
+  g2a o;
+  jac_to_aff(o, e);
+  H[i] = o;
+}
+
 // one wave per message (bls_w4.h: four row-distributed products per round), the smallest
 // launches: Q0 + Q1, the cofactor clearing and the affine conversion at ~0.5 us per round
 template <bool X>
@@ -195,8 +289,13 @@ void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   else if (n >= kLaneRegimeClear) {
     // Q is a scratch of the call (the map's output); its two slots per message carry the
     // points between the two chains
-    k_h2c_clear_lane_a<<<nblk(n), WG, 0, st>>>(const_cast<g2j *>(Q), n);
-    k_h2c_clear_lane_b<<<nblk(n), WG, 0, st>>>(Q, n, H);
+    if (g_lane_r28) {
+      k_h2c_clear_lane_a28<<<nblk(n), WG, 0, st>>>(const_cast<g2j *>(Q), n);
+      k_h2c_clear_lane_b28<<<nblk(n), WG, 0, st>>>(Q, n, H);
+    } else {
+      k_h2c_clear_lane_a<<<nblk(n), WG, 0, st>>>(const_cast<g2j *>(Q), n);
+      k_h2c_clear_lane_b<<<nblk(n), WG, 0, st>>>(Q, n, H);
+    }
   }
   else if (n <= g_row_clear_max)
     k_h2c_clear_row<<<nblk((size_t)n * 16), WG, 0, st>>>(Q, n, H);

@@ -7,7 +7,7 @@ namespace gbls {
 
 // Workgroup tree reduction of one Jacobian point per lane through LDS (result: lane 0)
 template <class F>
-__device__ void wg_reduce_jac(jac<F> &v) {
+__device__ __forceinline__ void wg_reduce_jac(jac<F> &v) {
   __shared__ jac<F> buf[WGR / 2];
   for (int w = WGR / 2; w > 0; w >>= 1) {
     __syncthreads();
@@ -199,7 +199,7 @@ HD void scalar_from_be32(uint32_t (&s)[8], const uint8_t *b) {
   }
 }
 template <class F>
-__device__ void mul_scalar256(jac<F> &r, const aff<F> &base, const uint32_t (&s)[8]) {
+__device__ __forceinline__ void mul_scalar256(jac<F> &r, const aff<F> &base, const uint32_t (&s)[8]) {
   jac<F> acc;
   jac_set_inf(acc);
   for (int i = 255; i >= 0; i--) {

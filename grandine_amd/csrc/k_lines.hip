@@ -10,6 +10,7 @@
 #define GBLS_GANG_LINES
 #include "bls_gang.h"
 #include "bls_w4.h"
+#include "bls_curve28.h"
 
 namespace gbls {
 
@@ -211,6 +212,65 @@ __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first,
   if (e1 < ML_EVENTS) Ts[pair] = T;
 }
 
+// The lane regime in radix 2^28 (bls_curve28.h line_dbl28 / line_add28: one v_mad_u64_u32 per
+// product term instead of a mad + carry pair), the default since r05 (g_lane_r28).  Q (affine,
+// engine form) is converted once; T runs in radix 2^28; every coefficient is stored as its
+// repacked limbs (store12: no conversion product), which an engine-form reader sees as the
+// coefficient times 2^8 -- one scalar for the whole line, removed by the final exponentiation
+// (as the W4 form's 2^64).  Q's coordinates wait in LDS for the 5 addition steps; between the
+// event slices of a sliced submission T is stored in engine form, as every other form does.
+__device__ __forceinline__ void put28(uint32_t *L, uint32_t np, uint32_t pair, int e, int c, const r28::fe2 &v) {
+  fp w;
+  r28::store12(w, v.c0);
+#pragma unroll
+  for (int i = 0; i < 12; i++) L[line_word(e, c, i, np, pair)] = w.l[i];
+  r28::store12(w, v.c1);
+#pragma unroll
+  for (int i = 0; i < 12; i++) L[line_word(e, c + 1, i, np, pair)] = w.l[i];
+}
+__global__ void __launch_bounds__(WG) k_lines_lane28(const g2a *H, uint32_t first, uint32_t count,
+                                                     uint32_t np, int e0, int e1, g2h *Ts, uint32_t *L) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t pair = first + i;
+  const g2a Q = H[pair];
+  if (aff_is_inf(Q)) {
+    lines_range(L, np, pair, Q, e0, e1, Ts);  // identity lines (engine form)
+    return;
+  }
+  __shared__ r28::fe2 qs[2 * WG];
+  r28::fe2 &qx = qs[threadIdx.x], &qy = qs[WG + threadIdx.x];
+  r28::g2h28 T;
+  r28::from_fp(T.x.c0, Q.x.c0);
+  r28::from_fp(T.x.c1, Q.x.c1);
+  r28::from_fp(T.y.c0, Q.y.c0);
+  r28::from_fp(T.y.c1, Q.y.c1);
+  qx = T.x;
+  qy = T.y;
+  if (e0 > 0) {  // T between slices is engine form whatever kernel form wrote it
+    const g2h &t = Ts[pair];
+    r28::from_fp(T.x.c0, t.x.c0), r28::from_fp(T.x.c1, t.x.c1);
+    r28::from_fp(T.y.c0, t.y.c0), r28::from_fp(T.y.c1, t.y.c1);
+    r28::from_fp(T.z.c0, t.z.c0), r28::from_fp(T.z.c1, t.z.c1);
+  } else {
+    r28::f_one(T.z);
+  }
+  for (int e = e0; e < e1; e++) {
+    const int el = e - e0;
+    auto put = [&](int c, const r28::fe2 &v) { put28(L, np, pair, el, c, v); };
+    if (ev_is_dbl(e))
+      r28::line_dbl28(T, put);
+    else
+      r28::line_add28(T, qx, qy, put);
+  }
+  if (e1 < ML_EVENTS) {
+    g2h &t = Ts[pair];
+    r28::to_fp(t.x.c0, T.x.c0), r28::to_fp(t.x.c1, T.x.c1);
+    r28::to_fp(t.y.c0, T.y.c0), r28::to_fp(t.y.c1, T.y.c1);
+    r28::to_fp(t.z.c0, T.z.c0), r28::to_fp(t.z.c1, T.z.c1);
+  }
+}
+
 // one wave per pair (bls_w4.h), the smallest launches: a doubling step is six rounds of four
 // row-distributed products, the six line words two more (canonical engine form, SoA as above)
 __device__ __forceinline__ void line_put_w4(const w4::Ctx &c, uint32_t *L, uint32_t np, uint32_t pair,
@@ -322,6 +382,8 @@ void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, 
   if (count <= kW4Max)
     (count <= w4::kExclusiveMaxWaves ? k_lines_w4<true> : k_lines_w4<false>)<<<count, 64, 0, st>>>(
         H, first, count, np, e0, e1, Ts, lines);
+  else if (count >= kLaneRegimeLines && g_lane_r28)
+    k_lines_lane28<<<nblk(count), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
   else if (count >= kLaneRegimeLines)
     k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
   else if (count <= kRowRegimeMax)

@@ -24,13 +24,34 @@ __device__ __forceinline__ void ml_eval(sp034 &s, const uint32_t *L, uint32_t np
   line_eval_s(s, L0, L2, L3, Pp);
 }
 
-// grid (ceil(ngroup / 64), e1 - e0); group g = (first plist index, stride, count); the
-// lines buffer holds events [e0, e1) at e - e0
+// One block per (group block gb of 64 groups, event el): nbx * ne blocks in a 1-D grid.  XCD
+// order (g_ml_xcd): the dispatcher deals blocks round-robin over the 8 XCDs (MI355X_MICROARCH
+// "Workgroup dispatch"), so block b's work index is remapped (bijectively) to give each XCD a
+// contiguous run of work with the event fastest: the ne blocks of a group block run together
+// on ONE XCD and read its pairs' G1 points from that XCD's L2 once, instead of every event
+// re-reading them from HBM (the r04 launch fetched 2.33 GB for 1.35 GB of lines).  Group g =
+// (first plist index, stride, count); the lines buffer holds events [e0, e0 + ne) at e - e0.
+__device__ __forceinline__ uint32_t xcd_work_index(uint32_t b, uint32_t nwg) {
+  const uint32_t xcd = b % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
 __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np, const g1s *P,
                                                  const uint32_t *plist, const uint32_t *grp,
-                                                 uint32_t ngroup, int e0, fp12 *V0) {
-  uint32_t g = blockIdx.x * WG + threadIdx.x;
-  int el = blockIdx.y, e = e0 + el;
+                                                 uint32_t ngroup, int e0, int ne, int xcd_order,
+                                                 fp12 *V0) {
+  const uint32_t nwg = gridDim.x;
+  uint32_t w = blockIdx.x, gb;
+  int el;
+  if (xcd_order) {
+    w = xcd_work_index(w, nwg);
+    gb = w / (uint32_t)ne;
+    el = (int)(w % (uint32_t)ne);
+  } else {  // the r04 order: event-major
+    gb = w % (nwg / (uint32_t)ne);
+    el = (int)(w / (nwg / (uint32_t)ne));
+  }
+  uint32_t g = gb * WG + threadIdx.x;
+  int e = e0 + el;
   if (g >= ngroup) return;
   uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
   sp034 sa, sb;
@@ -49,28 +70,79 @@ __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np,
   V0[(size_t)e * ngroup + g] = acc;
 }
 
-#ifdef GBLS_EXPERIMENTS  // measured slower; not in the shipped build
-// k_ml_group in radix-2^28 arithmetic (bls_field28.h; GBLS_ML_R28=1): same grid, same
-// inputs, and an output that differs from k_ml_group's by an Fp scalar (2^-16 per line and
-// 2^8 from the engine-form reading), which the final exponentiation removes
+// k_ml_group in radix-2^28 arithmetic (bls_field28.h), the default since r05: same grid and
+// inputs; the sparse products reduce ONCE per output Fp coordinate (fe12_mul_034_lazy: six
+// products per reduction, one v_mad_u64_u32 per term, no carry words), and the output differs
+// from the 32-bit kernel's by an Fp scalar (2^-16 per line and 2^8 from the engine-form reading),
+// which the final exponentiation removes.  g_ml_r28 = 0 (GBLS_ML_R28=0) runs the r04 kernel.
+// Registers: f (168) + the line (84) + three negated line operands; the three outputs the
+// in-place order parks live in LDS (fe12_mul_034_lazy_st, 84 words per lane), the line is
+// evaluated one component at a time (ml_eval28), and the result leaves as raw radix-2^28
+// words (k_ml_pack28 converts them): 256 VGPRs + ~140 AGPRs, no scratch.
+// the line of event e at pair `pair`, evaluated at its G1 point, in radix 2^28: one line
+// component (12 engine words) at a time, the next one's loads in flight during this one's
+// product, so at most two components and the point's current coordinate are live
 __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_t np, const g1s *P,
                                           uint32_t pair, int e) {
-  fp2 L0, L2, L3;
-  line_get(L, np, pair, e, L0, L2, L3);
-  const g1s &Pp = P[pair];
-  if (fp_is_zero(Pp.c))
+  const g1s *Pp = P + pair;
+  fp pc;
+#pragma unroll
+  for (int i = 0; i < 12; i++) pc.l[i] = Pp->c.l[i];
+  if (fp_is_zero(pc)) {
     r28::sp_identity(s);
-  else
-    r28::sp_from_engine(s, L0, L2, L3, Pp.x, Pp.y, Pp.c);
+    return;
+  }
+  r28::fe *out[6] = {&s.a0.c0, &s.a0.c1, &s.a2.c0, &s.a2.c1, &s.a3.c0, &s.a3.c1};
+  uint32_t cur[12], nxt[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, 0, i, np, pair)];
+  r28::fe q;
+  r28::repack_in(q, pc);
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) cur[i] = nxt[i];
+    if (c < 5) {
+#pragma unroll
+      for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, c + 1, i, np, pair)];
+    }
+    if (c == 2 || c == 4) {  // the point's x for L2, its y for L3
+      fp t;
+      const fp &src = c == 2 ? Pp->x : Pp->y;
+#pragma unroll
+      for (int i = 0; i < 12; i++) t.l[i] = src.l[i];
+      r28::repack_in(q, t);
+    }
+    asm volatile("" ::: "memory");
+    fp w;
+#pragma unroll
+    for (int i = 0; i < 12; i++) w.l[i] = cur[i];
+    r28::fe t;
+    r28::repack_in(t, w);
+    r28::mul(*out[c], t, q);
+    asm volatile("" ::: "memory");
+  }
 }
 __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t np, const g1s *P,
                                                    const uint32_t *plist, const uint32_t *grp,
-                                                   uint32_t ngroup, int e0, fp12 *V0) {
-  uint32_t g = blockIdx.x * WG + threadIdx.x;
-  int el = blockIdx.y, e = e0 + el;
+                                                   uint32_t ngroup, int e0, int ne, int xcd_order,
+                                                   uint32_t *V28) {
+  const uint32_t nwg = gridDim.x;
+  uint32_t w = blockIdx.x, gb;
+  int el;
+  if (xcd_order) {
+    w = xcd_work_index(w, nwg);
+    gb = w / (uint32_t)ne;
+    el = (int)(w % (uint32_t)ne);
+  } else {
+    gb = w % (nwg / (uint32_t)ne);
+    el = (int)(w / (nwg / (uint32_t)ne));
+  }
+  uint32_t g = gb * WG + threadIdx.x;
+  int e = e0 + el;
   if (g >= ngroup) return;
   uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
-  __shared__ uint32_t stash[154 * WG];
+  __shared__ uint32_t park[84 * WG];
   r28::sp sa, sb;
   r28::fe12 acc;
   ml_eval28(sa, L, np, P, plist[at], el);
@@ -78,18 +150,38 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
     r28::sp_to_fe12(acc, sa);
   } else {
     ml_eval28(sb, L, np, P, plist[at + stride], el);
-    r28::sp_mul_sp(acc, sa, sb);
+    r28::sp_mul_sp_lazy(acc, sa, sb);
     for (uint32_t j = 2; j < cnt; j++) {
       ml_eval28(sa, L, np, P, plist[at + j * stride], el);
-      r28::fe12_mul_034_st(acc, acc, sa, stash + threadIdx.x, WG);
+      r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
     }
   }
-  fp12 out;
-  r28::fe12_to_engine_scaled(out, acc);
-  V0[(size_t)e * ngroup + g] = out;
+  // raw radix-2^28 words, structure of arrays (word q of group g at (e * 168 + q) * ngroup + g:
+  // one coalesced dword per lane per store); k_ml_pack28 converts them to engine form
+  const uint32_t *ww = reinterpret_cast<const uint32_t *>(&acc);
+  uint32_t *o = V28 + (size_t)e * 168 * ngroup + g;
+#pragma unroll
+  for (int i = 0; i < 168; i++) o[(size_t)i * ngroup] = ww[i];
 }
 
-#endif  // GBLS_EXPERIMENTS
+// V28 (raw words of k_ml_group28, structure of arrays) -> V0 (engine-form fp12): one lane per
+// (event, group, coefficient): the canonical representative (values < 1.02 p), repacked
+__global__ void __launch_bounds__(WG) k_ml_pack28(const uint32_t *V28, uint32_t ngroup, int e0,
+                                                  uint32_t nvals, fp12 *V0) {
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= nvals * 12) return;
+  const uint32_t c = t % 12, v = t / 12, g = v % ngroup, e = e0 + v / ngroup;
+  const uint32_t *src = V28 + ((size_t)e * 168 + 14 * c) * ngroup + g;
+  r28::fe x;
+#pragma unroll
+  for (int i = 0; i < 14; i++) x.l[i] = src[(size_t)i * ngroup];
+  (void)r28::sub_p_if_geq(x);
+  fp o;
+  r28::repack_out(o, x);
+  uint32_t *dst = reinterpret_cast<uint32_t *>(V0 + (size_t)e * ngroup + g) + 12 * c;
+#pragma unroll
+  for (int i = 0; i < 12; i++) dst[i] = o.l[i];
+}
 
 // copy one Fp12 image global <-> LDS with all 64 lanes
 __device__ __forceinline__ void w12_load(uint32_t *dst, const fp12 *src) {
@@ -140,16 +232,17 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
 
 void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
                      const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
-                     int e1, fp12 *V0) {
+                     int e1, fp12 *V0, uint32_t *V28) {
   dim3 grid(nblk(ngroup), e1 - e0);
   if (!ngroup || e1 <= e0) return;
-#ifdef GBLS_EXPERIMENTS
-  if (g_ml_r28) {
-    k_ml_group28<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
+  const dim3 grid1(nblk(ngroup) * (uint32_t)(e1 - e0));
+  if (g_ml_r28 && V28) {
+    k_ml_group28<<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    const uint32_t nvals = ngroup * (uint32_t)(e1 - e0);
+    k_ml_pack28<<<nblk((size_t)nvals * 12), WG, 0, st>>>(V28, ngroup, e0, nvals, V0);
     return;
   }
-#endif
-  k_ml_group<<<grid, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, V0);
+  k_ml_group<<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V0);
 }
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout) {

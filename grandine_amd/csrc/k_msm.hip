@@ -39,7 +39,6 @@
 
 namespace gbls {
 
-constexpr int MSM_K = 16;  // points per chunk
 
 __device__ __forceinline__ int msm_digit(uint64_t k, int w, int c, uint32_t &carry) {
   uint64_t raw = (c * w < 64) ? (k >> (c * w)) & ((1ull << c) - 1) : 0;
@@ -90,8 +89,8 @@ __global__ void __launch_bounds__(WGR) k_msm_count(const g2a *sigs, const uint64
 
 // one workgroup of 1024 lanes: start[b] (exclusive scan of cnt), cur = start,
 // cstart[b] (exclusive scan of ceil(cnt / K)); start/cstart have nb + 1 entries
-__global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t *cnt, uint32_t nb, uint32_t *start,
-                                                   uint32_t *cur, uint32_t *cstart) {
+__global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t *cnt, uint32_t nb, uint32_t K,
+                                                   uint32_t *start, uint32_t *cur, uint32_t *cstart) {
   __shared__ uint32_t s_a[1024], s_b[1024];
   __shared__ uint32_t base_a, base_b;
   if (threadIdx.x == 0) {
@@ -101,7 +100,7 @@ __global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t *cnt, uint32_t
   __syncthreads();
   for (uint32_t off = 0; off < nb; off += 1024) {
     uint32_t b = off + threadIdx.x;
-    uint32_t x = b < nb ? cnt[b] : 0, y = (x + MSM_K - 1) / MSM_K;
+    uint32_t x = b < nb ? cnt[b] : 0, y = (x + K - 1) / K;
     s_a[threadIdx.x] = x;
     s_b[threadIdx.x] = y;
     __syncthreads();
@@ -159,7 +158,8 @@ __global__ void __launch_bounds__(WGR) k_msm_scatter(const g2a *sigs, const uint
 // wave boundary 64 w inside [cstart[b], cstart[b + 1]) (msm_bucket_sum).
 __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_t *list,
                                                   const uint32_t *start, const uint32_t *cstart,
-                                                  uint32_t nb, uint32_t max_chunks, g2j *chunk) {
+                                                  uint32_t nb, uint32_t max_chunks, uint32_t K,
+                                                  g2j *chunk) {
   // structure-of-arrays image of the wave's partials: word w of lane l at xs[w * WG + l], so a
   // wave's 64 lanes touch 64 consecutive words (distinct banks) on every store and load (the
   // array-of-structures image, 288-byte stride, put 16 lanes on each bank: 80 % of the LDS
@@ -181,8 +181,8 @@ __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_
       else
         hi = mid;
     }
-    uint32_t e0 = start[lo] + (j - cstart[lo]) * MSM_K;
-    uint32_t e1 = min(e0 + MSM_K, start[lo + 1]);
+    uint32_t e0 = start[lo] + (j - cstart[lo]) * K;
+    uint32_t e1 = min(e0 + K, start[lo + 1]);
     for (uint32_t e = e0; e < e1; e++) {
       uint32_t v = list[e];
       g2a p = sigs[v & 0x7fffffffu];
@@ -324,7 +324,10 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.tree = p.c == 13;
   p.extra = p.tree ? (uint32_t)p.W : ((uint32_t)p.W << (p.c - 1));
   p.nb = nseg * ((uint32_t)p.W << (p.c - 1));
-  p.max_chunks = (uint32_t)(((uint64_t)p.W * n + MSM_K - 1) / MSM_K) + p.nb;
+  // chunks of <= K points: K = 8 gives a C2 step's launch ~1800 waves (2 per SIMD; 884 with
+  // K = 16 left a quarter of the SIMDs idle at VALU busy 0.43)
+  p.K = g_msm_k;
+  p.max_chunks = (uint32_t)(((uint64_t)p.W * n + p.K - 1) / p.K) + p.nb;
   size_t o = 0;
   auto take = [&](size_t bytes) {
     size_t at = o;
@@ -360,11 +363,11 @@ void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
   (void)hipMemsetAsync(seg_err, 0, p.nseg * 4, st);
   k_msm_count<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, pks, pre,
                                             pre2, cnt, seg_err);
-  k_msm_scan<<<1, 1024, 0, st>>>(cnt, p.nb, start, cur, cstart);
+  k_msm_scan<<<1, 1024, 0, st>>>(cnt, p.nb, p.K, start, cur, cstart);
   k_msm_scatter<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, cur,
                                               list);
   k_msm_chunk<<<nblk(p.max_chunks), WG, 0, st>>>(sigs, list, start, cstart, p.nb, p.max_chunks,
-                                                 chunk);
+                                                 p.K, chunk);
   if (!p.tree) {
     k_msm_pairs<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, p.extra, n, seg_off,
                                            empty_is_error, P, H, seg_err);

@@ -2,8 +2,10 @@
 one the other GPU tests share): gbls_registry_set with GROWTH while registry-indexed
 verifications are still running on a device stream (VERDICT r04 "next 5").
 
-* 8 indexed multi_verify submissions of 8192 sets each are queued on one torch stream
-  (gbls_multi_verify_indexed_segments_device: asynchronous, reading the registry);
+* 16 indexed multi_verify submissions of 16384 sets each are queued on 4 torch streams
+  (gbls_multi_verify_indexed_segments_device: asynchronous, reading the registry; a context
+  recycles its staging buffer only after its previous call's uploads, so one stream alone
+  and each context has 4 staging buffers: ~60 ms of work stays queued);
 * registry_set then loads keys far past the table's capacity (the table is reallocated and the
   old one retired behind those readers on the GPU) and must return while the stream is still
   busy -- no device-wide synchronisation, no host wait for other callers' work;
@@ -30,7 +32,7 @@ def main():
     replicas = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     L = G.lib(0, replicas)
     dev = torch.device("cuda", 0)
-    n_reg, n, k = 4096, 8192, 8
+    n_reg, n, k, nst = 4096, 16384, 16, 4
     sks, comp = F.registry(n_reg, seed=b"async")
     assert not F.load_registry(comp).any()
     cap0 = L.gbls_registry_size()
@@ -45,20 +47,25 @@ def main():
     d_r = torch.from_numpy(np.array(F.rands(n, 3), dtype=np.uint64).view(np.int64)).to(dev)
     verdicts = torch.full((k,), -1, dtype=torch.int32, device=dev)
     off = G.u32_array([0, n])
-    s = torch.cuda.Stream(dev)
-    # warm-up (workspaces sized), then the timed queue
-    with torch.cuda.stream(s):
-        G.check(L.gbls_multi_verify_indexed_segments_device(
-            d_msgs.data_ptr(), d_sigs.data_ptr(), d_idx.data_ptr(), None, d_r.data_ptr(), n, off, 1,
-            verdicts.data_ptr(), ctypes.c_void_p(s.cuda_stream)), "warm")
-    s.synchronize()
+    streams = [torch.cuda.Stream(dev) for _ in range(nst)]
+    # warm-up (every stream's context sized), then the timed queue
+    for s in streams:
+        with torch.cuda.stream(s):
+            G.check(L.gbls_multi_verify_indexed_segments_device(
+                d_msgs.data_ptr(), d_sigs.data_ptr(), d_idx.data_ptr(), None, d_r.data_ptr(), n, off, 1,
+                verdicts.data_ptr(), ctypes.c_void_p(s.cuda_stream)), "warm")
+    torch.cuda.synchronize()
     verdicts.fill_(-1)
     torch.cuda.synchronize()
-    with torch.cuda.stream(s):
-        for j in range(k):
+    t_q = time.perf_counter()
+    for j in range(k):
+        s = streams[j % nst]
+        with torch.cuda.stream(s):
             G.check(L.gbls_multi_verify_indexed_segments_device(
                 d_msgs.data_ptr(), (d_bad if j % 3 == 1 else d_sigs).data_ptr(), d_idx.data_ptr(), None,
                 d_r.data_ptr(), n, off, 1, verdicts[j:].data_ptr(), ctypes.c_void_p(s.cuda_stream)), "queued")
+    enq_ms = 1e3 * (time.perf_counter() - t_q)
+    busy_before_set = any(not s.query() for s in streams)
     # growth while they run: 64 new keys at index 400000 (the table holds ~5k)
     new_sks, new_comp = F.registry(64, seed=b"async-new")
     first = 400_000
@@ -66,10 +73,11 @@ def main():
     t0 = time.perf_counter()
     rc = L.gbls_registry_set(first, G.buf(new_comp), 64, st)
     t_set = time.perf_counter() - t0
-    busy_after_set = not s.query()
-    s.synchronize()
+    busy_after_set = any(not s.query() for s in streams)
+    torch.cuda.synchronize()
     t_all = time.perf_counter() - t0
     res = {"rc": rc, "statuses": sorted(set(st)), "busy_after_set": busy_after_set,
+           "busy_before_set": busy_before_set, "enqueue_ms": round(enq_ms, 3),
            "set_ms": round(1e3 * t_set, 3), "queue_ms": round(1e3 * t_all, 3),
            "verdicts": verdicts.cpu().tolist(), "size": L.gbls_registry_size(), "cap0": cap0,
            "replicas": L.gbls_device_count()}

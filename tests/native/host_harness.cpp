@@ -120,15 +120,21 @@ int h_r28_tower_check(uint64_t seed, int rounds, int chain) {
     sp_mul_sp(ef, ea, eb);
     r28::sp_mul_sp(qf, qa, qb);
     bad += h_cmp12(ef, qf);
+    {  // the lazy sparse x sparse product (one reduction per output coordinate)
+      r28::fe12 ql;
+      r28::sp_mul_sp_lazy(ql, qa, qb);
+      bad += h_cmp12(ef, ql);
+    }
     for (int j = 0; j < chain; j++) {
       h_rand_fp2(ea.a0), h_rand_fp2(ea.a2), h_rand_fp2(ea.a3);
       h_to28(qa.a0, ea.a0), h_to28(qa.a2, ea.a2), h_to28(qa.a3, ea.a3);
       fp12_mul_034(ef, ef, ea);
-      if (j & 1) {
-        uint32_t st[154 * 3];
-        r28::fe12_mul_034_st(qf, qf, qa, st + 1, 3);
-      } else {
-        r28::fe12_mul_034(qf, qf, qa);
+      uint32_t st[154 * 3];
+      switch (j & 3) {  // every form, chained (each one's outputs are the next one's inputs)
+        case 0: r28::fe12_mul_034(qf, qf, qa); break;
+        case 1: r28::fe12_mul_034_st(qf, qf, qa, st + 1, 3); break;
+        case 2: r28::fe12_mul_034_lazy(qf, qa); break;
+        default: r28::fe12_mul_034_lazy_st(qf, qa, st + 2, 3); break;
       }
     }
     bad += h_cmp12(ef, qf);
@@ -152,6 +158,58 @@ int h_r28_tower_check(uint64_t seed, int rounds, int chain) {
       fp_mul(r, q0, *ev[i]);
       bad += h_fp_differs(l, r);
     }
+  }
+  return bad;
+}
+
+// the radix-2^28 Miller line steps (bls_curve28.h line_dbl28 / line_add28, k_lines_lane28)
+// against the engine's (bls_pairing.h line_dbl / line_add_aff) over the 68 events from a
+// random Q: every line coefficient and the final T equal as field elements
+int h_r28_lines_check(uint64_t seed) {
+  h_rng = seed;
+  g2a Q;
+  h_rand_fp2(Q.x), h_rand_fp2(Q.y);
+  g2h T;
+  T.x = Q.x, T.y = Q.y;
+  fp2_one(T.z);
+  r28::g2h28 T28;
+  r28::fe2 qx, qy;
+  h_to28(qx, Q.x), h_to28(qy, Q.y);
+  T28.x = qx, T28.y = qy;
+  r28::f_one(T28.z);
+  int bad = 0;
+  for (int e = 0; e < ML_EVENTS; e++) {
+    fp2 L[6], E[3];
+    auto put = [&](int c, const r28::fe2 &v) {
+      r28::to_fp(L[c].c0, v.c0);
+      r28::to_fp(L[c].c1, v.c1);
+    };
+    if (ev_is_dbl(e)) {
+      line_dbl(T, E[0], E[1], E[2]);
+      r28::line_dbl28(T28, put);
+    } else {
+      line_add_aff(T, Q, E[0], E[1], E[2]);
+      r28::line_add28(T28, qx, qy, put);
+    }
+    for (int k = 0; k < 3; k++)
+      bad += h_fp_differs(L[2 * k].c0, E[k].c0) + h_fp_differs(L[2 * k].c1, E[k].c1);
+    // the stored form: repacked radix-2^28 words read back (load12) are the same value
+    fp w;
+    r28::fe back;
+    r28::store12(w, T28.x.c0);
+    r28::load12(back, w);
+    fp a, b;
+    r28::to_fp(a, back);
+    r28::to_fp(b, T28.x.c0);
+    bad += h_fp_differs(a, b);
+  }
+  const fp2 *ev[3] = {&T.x, &T.y, &T.z};
+  const r28::fe2 *qv[3] = {&T28.x, &T28.y, &T28.z};
+  for (int k = 0; k < 3; k++) {
+    fp t0, t1;
+    r28::to_fp(t0, qv[k]->c0);
+    r28::to_fp(t1, qv[k]->c1);
+    bad += h_fp_differs(t0, ev[k]->c0) + h_fp_differs(t1, ev[k]->c1);
   }
   return bad;
 }

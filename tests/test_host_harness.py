@@ -247,10 +247,23 @@ def test_radix28_field_layer(H):
 
 def test_radix28_sparse_miller_products(H):
     """bls_field28.h's sparse Miller products (the r28 k_ml_group path) equal the engine's
-    (bls_pairing.h) on random operands, through 40-step dense x sparse chains; sp_from_engine
-    differs from line_eval_s by one scalar shared by all coefficients."""
+    (bls_pairing.h) on random operands, through 40-step dense x sparse chains that rotate over
+    every form (Karatsuba, Karatsuba with the LDS stash, and the k_ml_group28 lazy forms with one
+    reduction per output coordinate, in place, with and without parked outputs), and the lazy
+    sparse x sparse product; sp_from_engine differs from line_eval_s by one scalar shared by all
+    coefficients."""
     H.h_r28_tower_check.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
     assert H.h_r28_tower_check(7, 30, 40) == 0
+
+
+def test_radix28_miller_line_steps(H):
+    """The radix-2^28 line steps of k_lines_lane28 (bls_curve28.h line_dbl28 / line_add28, the
+    store-as-known order) equal the engine's line_dbl / line_add_aff (bls_pairing.h) at every
+    one of the 68 events from random points, coefficient by coefficient, and the running point
+    T at the end; the repacked storage form reads back as the same value."""
+    H.h_r28_lines_check.argtypes = [ctypes.c_uint64]
+    for seed in range(1, 9):
+        assert H.h_r28_lines_check(seed) == 0, seed
 
 
 def test_radix28_cofactor_clearing(H):
