@@ -47,6 +47,7 @@ uint32_t gbls::g_row_clear_max = gbls::kRowClearMax;
 uint32_t gbls::g_ml_r28 = 1;
 uint32_t gbls::g_msm_k = gbls::kMsmChunk;
 uint32_t gbls::g_ml_xcd = 1;
+uint32_t gbls::g_ml_dma = 0;
 uint32_t gbls::g_lane_r28 = 1;
 
 namespace {
@@ -428,6 +429,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_BLOCK_RESERVE")) g.block_reserve = std::atoi(e);
     if (const char *e = std::getenv("GBLS_BLOCK_HOLD")) g.block_hold = std::atoi(e) != 0;
     if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_ML_DMA")) g_ml_dma = (uint32_t)std::strtoul(e, nullptr, 10);
   }
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;

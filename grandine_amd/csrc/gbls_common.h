@@ -35,8 +35,9 @@ constexpr uint32_t kW4Max = GBLS_W4_MAX;
 constexpr uint32_t kRowClearMax = 2048;
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
 extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic (GBLS_ML_R28)
-constexpr uint32_t kMsmChunk = 8;        // k_msm_chunk: points summed per lane before the folds
+constexpr uint32_t kMsmChunk = 16;       // k_msm_chunk: points summed per lane before the folds
 extern uint32_t g_msm_k;                 // kMsmChunk unless GBLS_MSM_K is set
+extern uint32_t g_ml_dma;                // k_ml_group28: line staged in LDS by DMA loads (GBLS_ML_DMA)
 extern uint32_t g_ml_xcd;                // k_ml_group: XCD-grouped block order (GBLS_ML_XCD)
 extern uint32_t g_lane_r28;              // lane-regime clearing / lines in radix 2^28 (GBLS_LANE_R28)
 // line-coefficient buffer bound per submission (19.6 KB per pair: 4 GB = 214k pairs,

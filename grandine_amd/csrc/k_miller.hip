@@ -123,6 +123,59 @@ __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_
     asm volatile("" ::: "memory");
   }
 }
+typedef const void __attribute__((address_space(1))) *gptr_t;
+typedef void __attribute__((address_space(3))) *lptr_t;
+// LDS staging of the line (g_ml_dma, the default): the 72 line words of one pair's event into the wave's LDS stage (word w of lane l at
+// lbuf[w * WG + l]): global -> LDS DMA loads, no VGPR destination, one coalesced dword per lane
+__device__ __forceinline__ void ml_stage28(uint32_t *lbuf, const uint32_t *L, uint32_t np, uint32_t pair, int e) {
+#pragma unroll
+  for (int w = 0; w < 72; w++)
+    __builtin_amdgcn_global_load_lds((gptr_t)(L + line_word(e, w / 12, w % 12, np, pair)),
+                                     (lptr_t)(lbuf + w * WG), 4, 0, 0);
+}
+// the staged line evaluated at the pair's G1 point (loaded one pair ahead, ml_p_load), from
+// the LDS words
+struct MlP {
+  fp x, y, c;
+};
+__device__ __forceinline__ void ml_p_load(MlP &p, const g1s *P, uint32_t pair) {
+  const g1s *Pp = P + pair;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    p.c.l[i] = Pp->c.l[i];
+    p.x.l[i] = Pp->x.l[i];
+    p.y.l[i] = Pp->y.l[i];
+  }
+}
+__device__ __forceinline__ void ml_eval28_lds(r28::sp &s, const uint32_t *lb, const MlP &p) {
+  if (fp_is_zero(p.c)) {
+    r28::sp_identity(s);
+    return;
+  }
+  r28::fe *out[6] = {&s.a0.c0, &s.a0.c1, &s.a2.c0, &s.a2.c1, &s.a3.c0, &s.a3.c1};
+  r28::fe q;
+  r28::repack_in(q, p.c);
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    if (c == 2) r28::repack_in(q, p.x);
+    if (c == 4) r28::repack_in(q, p.y);
+    asm volatile("" ::: "memory");
+    fp w;
+#pragma unroll
+    for (int i = 0; i < 12; i++) w.l[i] = lb[(12 * c + i) * WG];
+    r28::fe t;
+    r28::repack_in(t, w);
+    r28::mul(*out[c], t, q);
+    asm volatile("" ::: "memory");
+  }
+}
+__device__ __forceinline__ void dma_wait() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+__device__ __forceinline__ void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <bool DMA>
 __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t np, const g1s *P,
                                                    const uint32_t *plist, const uint32_t *grp,
                                                    uint32_t ngroup, int e0, int ne, int xcd_order,
@@ -145,15 +198,60 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
   __shared__ uint32_t park[84 * WG];
   r28::sp sa, sb;
   r28::fe12 acc;
-  ml_eval28(sa, L, np, P, plist[at], el);
-  if (cnt == 1) {
-    r28::sp_to_fe12(acc, sa);
+  if constexpr (DMA) {
+    // pair j + 1's line is staged into LDS by DMA loads (no VGPR destinations) while pair j's
+    // product runs; the waits are vmcnt(0) + barrier before the LDS reads, lgkmcnt(0) after
+    // them (the next stage overwrites the buffer)
+    __shared__ uint32_t lbuf[72 * WG];
+    const uint32_t *lb = lbuf + threadIdx.x;
+    // the pair's G1 point is loaded with the stage (one pair ahead, into AGPRs); the next
+    // pair's index right after the stage's wait, so that the evaluation hides its latency
+    // (a loop-carried index load was waited at once: its VGPR -> AGPR copy)
+    MlP pp;
+    uint32_t pn = plist[at];
+    ml_stage28(lbuf, L, np, pn, el);
+    ml_p_load(pp, P, pn);
+    dma_wait();
+    pn = plist[at + (cnt > 1 ? stride : 0)];  // unconditional: a phi would wait on the load
+    ml_eval28_lds(sa, lb, pp);
+    lds_reads_done();
+    if (cnt == 1) {
+      r28::sp_to_fe12(acc, sa);
+    } else {
+      ml_stage28(lbuf, L, np, pn, el);
+      ml_p_load(pp, P, pn);
+      dma_wait();
+      pn = plist[at + (cnt > 2 ? 2 * stride : 0)];
+      ml_eval28_lds(sb, lb, pp);
+      lds_reads_done();
+      if (cnt > 2) {
+        ml_stage28(lbuf, L, np, pn, el);
+        ml_p_load(pp, P, pn);
+      }
+      r28::sp_mul_sp_lazy(acc, sa, sb);
+      for (uint32_t j = 2; j < cnt; j++) {
+        dma_wait();
+        pn = plist[at + (j + 1 < cnt ? (j + 1) * stride : 0)];
+        ml_eval28_lds(sa, lb, pp);
+        lds_reads_done();
+        if (j + 1 < cnt) {
+          ml_stage28(lbuf, L, np, pn, el);
+          ml_p_load(pp, P, pn);
+        }
+        r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
+      }
+    }
   } else {
-    ml_eval28(sb, L, np, P, plist[at + stride], el);
-    r28::sp_mul_sp_lazy(acc, sa, sb);
-    for (uint32_t j = 2; j < cnt; j++) {
-      ml_eval28(sa, L, np, P, plist[at + j * stride], el);
-      r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
+    ml_eval28(sa, L, np, P, plist[at], el);
+    if (cnt == 1) {
+      r28::sp_to_fe12(acc, sa);
+    } else {
+      ml_eval28(sb, L, np, P, plist[at + stride], el);
+      r28::sp_mul_sp_lazy(acc, sa, sb);
+      for (uint32_t j = 2; j < cnt; j++) {
+        ml_eval28(sa, L, np, P, plist[at + j * stride], el);
+        r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
+      }
     }
   }
   // raw radix-2^28 words, structure of arrays (word q of group g at (e * 168 + q) * ngroup + g:
@@ -165,12 +263,14 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
 }
 
 // V28 (raw words of k_ml_group28, structure of arrays) -> V0 (engine-form fp12): one lane per
-// (event, group, coefficient): the canonical representative (values < 1.02 p), repacked
+// (event, coefficient, group), the group fastest so that a wave's loads of one word are 64
+// consecutive dwords (the coefficient-fastest order read 14 scattered lines per lane: 5x the
+// algorithmic bytes in the r05 FETCH_SIZE pass); the canonical representative (< 1.02 p), repacked
 __global__ void __launch_bounds__(WG) k_ml_pack28(const uint32_t *V28, uint32_t ngroup, int e0,
                                                   uint32_t nvals, fp12 *V0) {
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
   if (t >= nvals * 12) return;
-  const uint32_t c = t % 12, v = t / 12, g = v % ngroup, e = e0 + v / ngroup;
+  const uint32_t g = t % ngroup, r = t / ngroup, c = r % 12, e = e0 + r / 12;
   const uint32_t *src = V28 + ((size_t)e * 168 + 14 * c) * ngroup + g;
   r28::fe x;
 #pragma unroll
@@ -237,7 +337,10 @@ void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g
   if (!ngroup || e1 <= e0) return;
   const dim3 grid1(nblk(ngroup) * (uint32_t)(e1 - e0));
   if (g_ml_r28 && V28) {
-    k_ml_group28<<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    if (g_ml_dma)
+      k_ml_group28<true><<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else
+      k_ml_group28<false><<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     const uint32_t nvals = ngroup * (uint32_t)(e1 - e0);
     k_ml_pack28<<<nblk((size_t)nvals * 12), WG, 0, st>>>(V28, ngroup, e0, nvals, V0);
     return;

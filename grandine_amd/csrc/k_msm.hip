@@ -183,9 +183,17 @@ __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_
     }
     uint32_t e0 = start[lo] + (j - cstart[lo]) * K;
     uint32_t e1 = min(e0 + K, start[lo + 1]);
+    // the next point's loads are issued before this point's addition: at one wave per SIMD the
+    // chain otherwise waits on every random-address load (VALU busy 0.43 in the r04 PMC pass)
+    uint32_t vn = list[e0];
+    g2a pn = sigs[vn & 0x7fffffffu];
     for (uint32_t e = e0; e < e1; e++) {
-      uint32_t v = list[e];
-      g2a p = sigs[v & 0x7fffffffu];
+      const uint32_t v = vn;
+      g2a p = pn;
+      if (e + 1 < e1) {
+        vn = list[e + 1];
+        pn = sigs[vn & 0x7fffffffu];
+      }
       if (v >> 31) fp2_neg(p.y, p.y);
       jac_add_aff(acc, acc, p);
     }
@@ -324,8 +332,9 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.tree = p.c == 13;
   p.extra = p.tree ? (uint32_t)p.W : ((uint32_t)p.W << (p.c - 1));
   p.nb = nseg * ((uint32_t)p.W << (p.c - 1));
-  // chunks of <= K points: K = 8 gives a C2 step's launch ~1800 waves (2 per SIMD; 884 with
-  // K = 16 left a quarter of the SIMDs idle at VALU busy 0.43)
+  // chunks of <= K points (GBLS_MSM_K; measured r05: K = 8 fills the chip with ~1700 waves but
+  // VALU busy stays at 0.43 -- the chunk loop waits on its point loads, not on SIMDs -- and the
+  // larger folds cost 2.4 % of C2; K = 4 costs 5 %: K = 16 stays)
   p.K = g_msm_k;
   p.max_chunks = (uint32_t)(((uint64_t)p.W * n + p.K - 1) / p.K) + p.nb;
   size_t o = 0;

@@ -2,10 +2,9 @@
 one the other GPU tests share): gbls_registry_set with GROWTH while registry-indexed
 verifications are still running on a device stream (VERDICT r04 "next 5").
 
-* 16 indexed multi_verify submissions of 16384 sets each are queued on 4 torch streams
-  (gbls_multi_verify_indexed_segments_device: asynchronous, reading the registry; a context
-  recycles its staging buffer only after its previous call's uploads, so one stream alone
-  and each context has 4 staging buffers: ~60 ms of work stays queued);
+* two indexed multi_verify submissions of 131072 sets each (~30 ms of GPU work apiece) are
+  queued on two torch streams (gbls_multi_verify_indexed_segments_device: asynchronous, reading
+  the registry), the second with one swapped signature;
 * registry_set then loads keys far past the table's capacity (the table is reallocated and the
   old one retired behind those readers on the GPU) and must return while the stream is still
   busy -- no device-wide synchronisation, no host wait for other callers' work;
@@ -32,7 +31,7 @@ def main():
     replicas = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     L = G.lib(0, replicas)
     dev = torch.device("cuda", 0)
-    n_reg, n, k, nst = 4096, 16384, 16, 4
+    n_reg, n, k, nst = 4096, 131072, 2, 2
     sks, comp = F.registry(n_reg, seed=b"async")
     assert not F.load_registry(comp).any()
     cap0 = L.gbls_registry_size()
@@ -55,6 +54,7 @@ def main():
                 d_msgs.data_ptr(), d_sigs.data_ptr(), d_idx.data_ptr(), None, d_r.data_ptr(), n, off, 1,
                 verdicts.data_ptr(), ctypes.c_void_p(s.cuda_stream)), "warm")
     torch.cuda.synchronize()
+    new_sks, new_comp = F.registry(64, seed=b"async-new")
     verdicts.fill_(-1)
     torch.cuda.synchronize()
     t_q = time.perf_counter()
@@ -66,8 +66,7 @@ def main():
                 d_r.data_ptr(), n, off, 1, verdicts[j:].data_ptr(), ctypes.c_void_p(s.cuda_stream)), "queued")
     enq_ms = 1e3 * (time.perf_counter() - t_q)
     busy_before_set = any(not s.query() for s in streams)
-    # growth while they run: 64 new keys at index 400000 (the table holds ~5k)
-    new_sks, new_comp = F.registry(64, seed=b"async-new")
+    # growth while they run: 64 new keys at index 400000 (the table holds ~5k), made beforehand
     first = 400_000
     st = (ctypes.c_int32 * 64)()
     t0 = time.perf_counter()

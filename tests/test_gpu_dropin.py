@@ -264,7 +264,7 @@ def test_registry_growth_during_inflight_verifies_subprocess(replicas):
     res = json.loads(out.stdout.strip().splitlines()[-1])
     print(res)
     assert res["rc"] == 0 and res["statuses"] == [0] and res["replicas"] == replicas
-    assert res["verdicts"] == [0 if j % 3 != 1 else 5 for j in range(16)]
+    assert res["verdicts"] == [0, 5]
     # no device-wide stall and no wait for other callers' work inside registry_set: it returns
     # while the queued verifications still run (its own small kernels only need free SIMDs)
     assert res["busy_before_set"] and res["busy_after_set"], res

@@ -303,6 +303,24 @@ def test_bucket_msm_parity_subprocess():
     assert res["zero_scalar"] == 5
 
 
+@pytest.mark.parametrize("knobs", [["GBLS_ML_DMA=1"], ["GBLS_ML_R28=0"], ["GBLS_LANE_R28=0"]],
+                         ids=["ml-lds-dma", "ml-radix32", "lanes-radix32"])
+def test_kernel_variants_subprocess(knobs):
+    """The non-default kernel forms an operator can select (k_ml_group28 with the line staged
+    in LDS by DMA loads; the 32-bit-limb k_ml_group; the 32-bit-limb line / cofactor lanes):
+    golden multi_verify verdicts, 4096-set batches equal to the C oracle's, and a 4-segment
+    batch that flags exactly its corrupted segment (tests/gpu_knobs.py, its own engine)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_knobs.py")] + knobs,
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["knobs"] == knobs and all(res["golden"]), res
+    for name, gpu, ref in res["c2"]:
+        assert gpu == ref, (name, gpu, ref)
+    assert [x[1] for x in res["c2"]] == [True, False, False]
+    assert res["segments"] == [0, 0, 5, 0]
+
+
 def test_sliced_lines_subprocess():
     """Event-sliced Miller lines (GBLS_LINE_BUDGET_MB=16: a 4096-set batch in slices of
     a few events, the running points in HBM between slices): single-batch verdicts equal
