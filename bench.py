@@ -426,8 +426,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    enq = []  # host time of each step's enqueue (the device entry points return before the GPU work)
     for k in range(args.steps):
+        te = time.perf_counter()
         run(k)
+        enq.append(time.perf_counter() - te)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -535,6 +538,8 @@ def main():
                            "batches_per_step": getattr(leg, "segments", 1), "streams_in_flight": D,
                            "parallelism": "shard sets, RCCL all-gather of Fp12 partials" if world > 1 else "1 GPU"},
                 "roofline": roof, "cpu_baseline": cpu}
+        line["host_enqueue_ms"] = {"p50": round(sorted(enq)[len(enq) // 2] * 1e3, 3),
+                                   "max": round(max(enq) * 1e3, 3)}
         if cfg in ("C2", "C4", "C5"):
             line["pairings_per_s"] = round((total_units + world * leg.segments) * args.steps / dt, 1)
         if single:

@@ -2,6 +2,8 @@
 // engine's one-lane formulas (bls_curve.h / bls_hash.h / bls_pairing.h) on points r G2, plus
 // the latency of the chains the latency regime runs (doubling, cofactor clearing, Miller
 // lines).
+// With a file argument it also writes every W4 result (engine words) for the independent
+// Python-integer check tools/ubench/w4_check.py (oracle/bls12_381.py arithmetic).
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o tools/ubench/_bin/w4_check tools/ubench/w4_check.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,12 +41,25 @@ __device__ void store_j(const w4::Ctx &c, g2j *o, const w4::J &p) {
 // failure bits per wave: 1 gather, 2 dbl, 4 add, 8 add(P,P), 16 add(P,-P), 32 add(inf,Q),
 // 64 psi, 128 psi2, 256 [|x|]P, 512 clear, 1024 affine of clear, 2048 line_dbl, 4096 line_add,
 // 8192 madd, 16384 32-bit scalar chain, 32768 projective addition step
-__global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *fails) {
+// Dump slots (w4_check DUMPFILE: every W4 result, engine words, for tools/ubench/w4_check.py's
+// independent Python-integer recomputation from the seeds): see DUMP_NAMES there.
+constexpr int kDumpSlots = 16;
+__device__ void dump_words(uint32_t *dst, const void *src, int nwords) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(src);
+  for (int i = threadIdx.x; i < nwords; i += 64) dst[i] = w[i];
+}
+__global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *fails, g2j *dump) {
   w4::Ctx c;
   w4::init(c);
   __shared__ g2j out;
   __shared__ g2a outa;
   uint32_t f = 0;
+  g2j *dd = dump ? dump + (size_t)blockIdx.x * kDumpSlots : nullptr;
+  auto put = [&](int slot, const void *v, int nwords) {
+    __syncthreads();
+    if (dd) dump_words(reinterpret_cast<uint32_t *>(dd + slot), v, nwords);
+    __syncthreads();
+  };
   // gather
   {
     uint32_t o0, o1, o2, o3;
@@ -65,15 +80,18 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
   // dbl
   w4::dbl(c, jr, jp);
   store_j(c, &out, jr);
+  put(0, &out, 72);
   jac_dbl(R, P);
   if (!same(R)) f |= 2;
   // add
   w4::add(c, jr, jp, jq);
   store_j(c, &out, jr);
+  put(1, &out, 72);
   jac_add(R, P, Q);
   if (!same(R)) f |= 4;
   w4::add(c, jr, jp, jp);
   store_j(c, &out, jr);
+  put(2, &out, 72);
   jac_dbl(R, P);
   if (!same(R)) f |= 8;
   {
@@ -90,22 +108,27 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
   }
   w4::psi<10>(c, jr, jp);
   store_j(c, &out, jr);
+  put(3, &out, 72);
   g2_psi(R, P);
   if (!same(R)) f |= 64;
   w4::psi2(c, jr, jp);
   store_j(c, &out, jr);
+  put(4, &out, 72);
   g2_psi2(R, P);
   if (!same(R)) f |= 128;
   w4::mul_by_xabs(c, jr, jp);
   store_j(c, &out, jr);
+  put(5, &out, 72);
   mul_by_xabs(R, P);
   if (!same(R)) f |= 256;
   w4::clear_cofactor(c, jr, jp);
   store_j(c, &out, jr);
+  put(6, &out, 72);
   clear_cofactor_g2(R, P);
   if (!same(R)) f |= 512;
   w4::store_affine(c, &outa, jr);
   __syncthreads();
+  put(7, &outa, 48);
   {
     g2a want;
     jac_to_aff(want, R);
@@ -143,6 +166,8 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
     w4::store4(c, l3.c0, l3.c1, l3.c0, l3.c1, ll[2].c0.l, ll[2].c1.l, ll[2].c0.l, ll[2].c1.l);
     store_j(c, &tt, jt);
     __syncthreads();
+    put(8, &tt, 72);
+    put(9, ll, 72);
     // the row engine keeps the lane formulas' exact values mod p
     if (!(fp2_eq(ll[0], L0) && fp2_eq(ll[1], L2) && fp2_eq(ll[2], L3) && fp2_eq(tt.x, T.x) &&
           fp2_eq(tt.y, T.y) && fp2_eq(tt.z, T.z)))
@@ -154,6 +179,8 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
     w4::store4(c, l3.c0, l3.c1, l3.c0, l3.c1, ll[2].c0.l, ll[2].c1.l, ll[2].c0.l, ll[2].c1.l);
     store_j(c, &tt, jt);
     __syncthreads();
+    put(10, &tt, 72);
+    put(11, ll, 72);
     if (!(fp2_eq(ll[0], L0) && fp2_eq(ll[1], L2) && fp2_eq(ll[2], L3) && fp2_eq(tt.x, T.x) &&
           fp2_eq(tt.y, T.y) && fp2_eq(tt.z, T.z)))
       f |= 4096;
@@ -166,6 +193,7 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
     w4::load(c, jqa, qa);
     w4::madd(c, jr, jp, jqa);
     store_j(c, &out, jr);
+    put(12, &out, 72);
     jac_add_aff(R, P, qa);
     if (!same(R)) f |= 8192;
     const uint64_t k = (s * 0x2545F4914F6CDD1Dull) >> 32 | 1;
@@ -179,6 +207,7 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
       if ((k >> bit) & 1) w4::madd(c, acc, acc, jqa);
     }
     store_j(c, &out, acc);
+    put(13, &out, 72);
     mul_u64(R, qa, k);
     if (!same(R)) f |= 16384;
   }
@@ -211,6 +240,8 @@ __global__ void __launch_bounds__(64) k_check(const uint64_t *seeds, uint32_t *f
     w4::store4(c, l3.c0, l3.c1, l3.c0, l3.c1, ll[2].c0.l, ll[2].c1.l, ll[2].c0.l, ll[2].c1.l);
     store_j(c, &tt, jt);
     __syncthreads();
+    put(14, &tt, 72);
+    put(15, ll, 72);
     fp2 a, b;
     bool ok = true;
     // same homogeneous point: X Z' = X' Z, Y Z' = Y' Z
@@ -255,7 +286,7 @@ __global__ void __launch_bounds__(64) k_time(const uint64_t *seeds, g2a *out, ui
   }
 }
 
-int main() {
+int main(int argc, char **argv) {
   const int n = 64;
   uint64_t hs[n];
   for (int i = 0; i < n; i++) hs[i] = 0x9E3779B97F4A7C15ull * (i + 1) ^ (0xabcdefull << (i % 17));
@@ -264,8 +295,22 @@ int main() {
   CHK(hipMalloc(&ds, sizeof hs));
   CHK(hipMalloc(&df, n * 4));
   CHK(hipMemcpy(ds, hs, sizeof hs, hipMemcpyHostToDevice));
-  k_check<<<n, 64>>>(ds, df);
+  g2j *ddump = nullptr;
+  if (argc > 1) CHK(hipMalloc(&ddump, (size_t)n * kDumpSlots * sizeof(g2j)));
+  k_check<<<n, 64>>>(ds, df, ddump);
   CHK(hipDeviceSynchronize());
+  if (ddump) {  // the seeds, then every block's slots (tools/ubench/w4_check.py)
+    const size_t bytes = (size_t)n * kDumpSlots * sizeof(g2j);
+    void *h = malloc(bytes);
+    CHK(hipMemcpy(h, ddump, bytes, hipMemcpyDeviceToHost));
+    FILE *fo = fopen(argv[1], "wb");
+    if (!fo || fwrite(hs, sizeof hs, 1, fo) != 1 || fwrite(h, bytes, 1, fo) != 1) {
+      fprintf(stderr, "cannot write %s\n", argv[1]);
+      return 2;
+    }
+    fclose(fo);
+    free(h);
+  }
   uint32_t hf[n];
   CHK(hipMemcpy(hf, df, sizeof hf, hipMemcpyDeviceToHost));
   int bad = 0;
