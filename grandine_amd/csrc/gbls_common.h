@@ -35,7 +35,13 @@ constexpr uint32_t kW4Max = GBLS_W4_MAX;
 constexpr uint32_t kRowClearMax = 2048;
 extern uint32_t g_row_clear_max;         // kRowClearMax unless GBLS_ROW_CLEAR_MAX is set
 extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic (GBLS_ML_R28)
-constexpr uint32_t kMsmChunk = 16;       // k_msm_chunk: points summed per lane before the folds
+// k_msm_chunk: points summed per lane (mixed additions).  r05 (partials folded by k_msm_fold):
+// C2 4.25 / 4.27M at K = 16 (884 waves), 4.18 / 4.24M at K = 8 (1716), 4.22 / 4.18M at K = 6
+// (2271) -- within noise; the side-stream MSM overlaps the main chain, so its fill is not the
+// step's bound.  GBLS_MSM_K selects another K.
+constexpr uint32_t kMsmChunk = 16;
+constexpr int kMsmFoldLevels = 3;        // k_msm_fold: pairwise levels over each bucket's partials
+constexpr uint32_t kMsmFold = 1u << kMsmFoldLevels;  // chunk partials per fold group
 extern uint32_t g_msm_k;                 // kMsmChunk unless GBLS_MSM_K is set
 extern uint32_t g_ml_dma;                // k_ml_group28: line staged in LDS by DMA loads (GBLS_ML_DMA)
 extern uint32_t g_ml_xcd;                // k_ml_group: XCD-grouped block order (GBLS_ML_XCD)
@@ -105,9 +111,10 @@ struct MsmPlan {
   uint32_t nb;          // buckets (nseg * W * 2^(c-1))
   uint32_t max_chunks;  // bound on the chunk count (grid of the chunk kernel)
   uint32_t K;           // points per chunk
+  uint32_t max_folds;   // bound on the level-0 fold-pair count (grid of the fold kernels)
   bool tree;            // per-window bucket trees (c = 13) or per-bucket pairs (c = 5)
   uint32_t extra;       // extra Miller pairs per segment: W (tree) or W * 2^(c-1)
-  size_t o_cnt, o_start, o_cur, o_cstart, o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
+  size_t o_cnt, o_start, o_cur, o_cstart, o_fstart[kMsmFoldLevels], o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
 };
 // default: segments at least this large use the bucket MSM (2048 -> 4096 in r04: a C4 epoch of
 // 2048-set segments ran 542-572k sets/s with per-set products vs 375-390k with the MSM,

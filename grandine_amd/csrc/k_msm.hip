@@ -9,11 +9,18 @@
 // Signed c-bit digits, W = 65 / c windows, B = 2^(c-1) buckets per window and segment
 // (digit d != 0 adds sign(d) sig into bucket |d| - 1 of its segment's window):
 //   1 k_msm_count    lane per set: bucket histogram (atomics), segment error flags
-//   2 k_msm_scan     one workgroup: bucket starts, chunk starts (K entries per chunk)
+//   2 k_msm_scan     one workgroup: bucket starts, chunk starts (K entries per chunk), and
+//                    per fold level l the bucket's pair starts (2^(l+1) chunks per pair)
 //   3 k_msm_scatter  lane per set: (set | sign) into its buckets' lists
-//   4 k_msm_chunk    lane per chunk: sum of <= K affine points (mixed additions), then a
-//                    segmented fold of the wave's chunks by bucket through LDS (one
-//                    partial per bucket and wave; the bucket's reader adds them up)
+//   4 k_msm_chunk    lane per chunk: sum of <= K affine points (mixed additions), one partial
+//   4b k_msm_fold    kMsmFoldLevels launches, lane per pair of one bucket's partials at
+//                    level l: partial[j] += partial[j + 2^l] (full Jacobian additions), so
+//                    each run of kMsmFold partials ends summed in its first; the bucket's
+//                    reader adds the runs' sums (msm_bucket_sum)
+// (r05: the chunk kernel no longer folds its wave's partials through LDS -- log2(run) levels
+// of additions at whole-wave cost with most lanes masked off; the fold levels are their own
+// launches, every lane one addition, so K can be small: GBLS_MSM_K = 8 gives ~1.7k chunk
+// waves against 884 at K = 16, VERDICT r04 item 4, at the same C2 rate)
 // The bucket sums X_{w,b} never go through a Horner chain of 60 doublings.  The weights
 // move to the G1 side of the pairing instead, where they are constants:
 //   e(-g1, S) = prod_{w,b} e(-[(b+1) 2^(c w)] g1, X_{w,b}),
@@ -88,46 +95,56 @@ __global__ void __launch_bounds__(WGR) k_msm_count(const g2a *sigs, const uint64
 }
 
 // one workgroup of 1024 lanes: start[b] (exclusive scan of cnt), cur = start,
-// cstart[b] (exclusive scan of ceil(cnt / K)); start/cstart have nb + 1 entries
+// cstart[b] (exclusive scan of ceil(cnt / K)), fstart[l][b] (exclusive scan of the bucket's
+// level-l fold pairs, floor((ceil(cnt / K) + 2^l - 1) / 2^(l+1)) -- pairs whose second
+// partial exists); start/cstart/fstart[l] have nb + 1 entries
+struct MsmFoldStarts {
+  uint32_t *l[kMsmFoldLevels];
+};
 __global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t *cnt, uint32_t nb, uint32_t K,
-                                                   uint32_t *start, uint32_t *cur, uint32_t *cstart) {
-  __shared__ uint32_t s_a[1024], s_b[1024];
-  __shared__ uint32_t base_a, base_b;
-  if (threadIdx.x == 0) {
-    base_a = 0;
-    base_b = 0;
-  }
+                                                   uint32_t *start, uint32_t *cur,
+                                                   uint32_t *cstart, MsmFoldStarts fs) {
+  constexpr int NS = 2 + kMsmFoldLevels;
+  __shared__ uint32_t sv[NS][1024];
+  __shared__ uint32_t base[NS];
+  if (threadIdx.x < NS) base[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t off = 0; off < nb; off += 1024) {
     uint32_t b = off + threadIdx.x;
-    uint32_t x = b < nb ? cnt[b] : 0, y = (x + K - 1) / K;
-    s_a[threadIdx.x] = x;
-    s_b[threadIdx.x] = y;
+    uint32_t v[NS];
+    v[0] = b < nb ? cnt[b] : 0;
+    v[1] = (v[0] + K - 1) / K;
+#pragma unroll
+    for (int l = 0; l < kMsmFoldLevels; l++) v[2 + l] = (v[1] + (1u << l) - 1) >> (l + 1);
+#pragma unroll
+    for (int q = 0; q < NS; q++) sv[q][threadIdx.x] = v[q];
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
-      uint32_t xa = threadIdx.x >= d ? s_a[threadIdx.x - d] : 0;
-      uint32_t xb = threadIdx.x >= d ? s_b[threadIdx.x - d] : 0;
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scans
+      uint32_t x[NS];
+#pragma unroll
+      for (int q = 0; q < NS; q++) x[q] = threadIdx.x >= d ? sv[q][threadIdx.x - d] : 0;
       __syncthreads();
-      s_a[threadIdx.x] += xa;
-      s_b[threadIdx.x] += xb;
+#pragma unroll
+      for (int q = 0; q < NS; q++) sv[q][threadIdx.x] += x[q];
       __syncthreads();
     }
     if (b < nb) {
-      uint32_t sa = base_a + s_a[threadIdx.x] - x, sb = base_b + s_b[threadIdx.x] - y;
+      const uint32_t sa = base[0] + sv[0][threadIdx.x] - v[0];
       start[b] = sa;
       cur[b] = sa;
-      cstart[b] = sb;
+      cstart[b] = base[1] + sv[1][threadIdx.x] - v[1];
+#pragma unroll
+      for (int l = 0; l < kMsmFoldLevels; l++) fs.l[l][b] = base[2 + l] + sv[2 + l][threadIdx.x] - v[2 + l];
     }
     __syncthreads();
-    if (threadIdx.x == 1023) {
-      base_a += s_a[1023];
-      base_b += s_b[1023];
-    }
+    if (threadIdx.x < NS) base[threadIdx.x] += sv[threadIdx.x][1023];
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    start[nb] = base_a;
-    cstart[nb] = base_b;
+    start[nb] = base[0];
+    cstart[nb] = base[1];
+#pragma unroll
+    for (int l = 0; l < kMsmFoldLevels; l++) fs.l[l][nb] = base[2 + l];
   }
 }
 
@@ -150,79 +167,65 @@ __global__ void __launch_bounds__(WGR) k_msm_scatter(const g2a *sigs, const uint
   }
 }
 
-// chunk j: sum of <= K affine points of one bucket (found by binary search over cstart),
-// then, within the wave, a segmented pairwise fold of the wave's chunks by bucket: every
-// bucket's chunks inside one wave end up summed in its first chunk there (levels only
-// while some run of same-bucket chunks in the wave is longer than the step).  A bucket
-// thus leaves one partial per wave it touches, at its first chunk cstart[b] and at each
-// wave boundary 64 w inside [cstart[b], cstart[b + 1]) (msm_bucket_sum).
+// the largest b with tab[b] <= j (tab has nb + 1 nondecreasing entries, tab[0] = 0)
+__device__ __forceinline__ uint32_t msm_owner(const uint32_t *tab, uint32_t nb, uint32_t j) {
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (tab[mid] <= j)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// chunk j: sum of <= K affine points of one bucket (found by binary search over cstart), one
+// partial per chunk
 __global__ void __launch_bounds__(WG) k_msm_chunk(const g2a *sigs, const uint32_t *list,
                                                   const uint32_t *start, const uint32_t *cstart,
                                                   uint32_t nb, uint32_t max_chunks, uint32_t K,
                                                   g2j *chunk) {
-  // structure-of-arrays image of the wave's partials: word w of lane l at xs[w * WG + l], so a
-  // wave's 64 lanes touch 64 consecutive words (distinct banks) on every store and load (the
-  // array-of-structures image, 288-byte stride, put 16 lanes on each bank: 80 % of the LDS
-  // cycles were conflicts)
-  constexpr int NW = sizeof(g2j) / 4;
-  __shared__ uint32_t xs[NW * WG];
-  const uint32_t lane = threadIdx.x, base = blockIdx.x * WG;
-  const uint32_t j = base + lane, total = cstart[nb];
-  const bool live = j < max_chunks && j < total;
+  const uint32_t j = blockIdx.x * WG + threadIdx.x;
+  if (j >= max_chunks || j >= cstart[nb]) return;
+  const uint32_t b = msm_owner(cstart, nb, j);
+  const uint32_t e0 = start[b] + (j - cstart[b]) * K;
+  const uint32_t e1 = min(e0 + K, start[b + 1]);
   g2j acc;
   jac_set_inf(acc);
-  uint32_t lo = 0;
-  if (live) {
-    uint32_t hi = nb;  // largest b with cstart[b] <= j
-    while (hi - lo > 1) {
-      uint32_t mid = (lo + hi) >> 1;
-      if (cstart[mid] <= j)
-        lo = mid;
-      else
-        hi = mid;
+  // the next point's loads are issued before this point's addition: at one wave per SIMD the
+  // chain otherwise waits on every random-address load
+  uint32_t vn = list[e0];
+  g2a pn = sigs[vn & 0x7fffffffu];
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint32_t v = vn;
+    g2a p = pn;
+    if (e + 1 < e1) {
+      vn = list[e + 1];
+      pn = sigs[vn & 0x7fffffffu];
     }
-    uint32_t e0 = start[lo] + (j - cstart[lo]) * K;
-    uint32_t e1 = min(e0 + K, start[lo + 1]);
-    // the next point's loads are issued before this point's addition: at one wave per SIMD the
-    // chain otherwise waits on every random-address load (VALU busy 0.43 in the r04 PMC pass)
-    uint32_t vn = list[e0];
-    g2a pn = sigs[vn & 0x7fffffffu];
-    for (uint32_t e = e0; e < e1; e++) {
-      const uint32_t v = vn;
-      g2a p = pn;
-      if (e + 1 < e1) {
-        vn = list[e + 1];
-        pn = sigs[vn & 0x7fffffffu];
-      }
-      if (v >> 31) fp2_neg(p.y, p.y);
-      jac_add_aff(acc, acc, p);
-    }
+    if (v >> 31) fp2_neg(p.y, p.y);
+    jac_add_aff(acc, acc, p);
   }
-  // this lane's position in its bucket's run inside the wave, and the run's end (lanes)
-  const uint32_t first = live ? (cstart[lo] > base ? cstart[lo] - base : 0u) : lane;
-  const uint32_t end = live ? min((uint32_t)WG, cstart[lo + 1] - base) : lane + 1;
-  const uint32_t k = lane - first;
-  uint32_t run = end - first;  // wave maximum of the run lengths
-  for (int o = 32; o >= 1; o >>= 1) run = max(run, (uint32_t)__shfl_xor((int)run, o));
-  for (uint32_t st = 1; st < run; st <<= 1) {
-    const uint32_t *aw = reinterpret_cast<const uint32_t *>(&acc);
-#pragma unroll
-    for (int w = 0; w < NW; w++) xs[w * WG + lane] = aw[w];
-    __syncthreads();
-    if ((k & (2 * st - 1)) == 0 && lane + st < end) {
-      g2j x;
-      uint32_t *xw = reinterpret_cast<uint32_t *>(&x);
-#pragma unroll
-      for (int w = 0; w < NW; w++) xw[w] = xs[w * WG + lane + st];
-      jac_add(acc, acc, x);
-    }
-    __syncthreads();
-  }
-  if (live && k == 0) chunk[j] = acc;
+  chunk[j] = acc;
 }
 
-// sum of bucket b: its first chunk's partial plus the partials at the chunk waves' starts
-// inside the bucket's chunk range (k_msm_chunk)
+// fold level l, pair t of bucket b = owner: partial[j] += partial[j + 2^l] for
+// j = cstart[b] + (t - fstart[b]) 2^(l+1) (only pairs whose second partial exists are counted)
+__global__ void __launch_bounds__(WG) k_msm_fold(const uint32_t *cstart, const uint32_t *fstart,
+                                                 uint32_t nb, uint32_t max_pairs, int l,
+                                                 g2j *chunk) {
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= max_pairs || t >= fstart[nb]) return;
+  const uint32_t b = msm_owner(fstart, nb, t);
+  const uint32_t j = cstart[b] + ((t - fstart[b]) << (l + 1));
+  g2j x = chunk[j], y = chunk[j + (1u << l)];
+  jac_add(x, x, y);
+  chunk[j] = x;
+}
+
+// sum of bucket b: its fold groups' sums (k_msm_fold), at every kMsmFold-th chunk partial of
+// the bucket's chunk range
 __device__ __forceinline__ void msm_bucket_sum(g2j &x, const g2j *chunk, const uint32_t *cstart,
                                                uint32_t b) {
   const uint32_t c0 = cstart[b], c1 = cstart[b + 1];
@@ -231,7 +234,7 @@ __device__ __forceinline__ void msm_bucket_sum(g2j &x, const g2j *chunk, const u
     return;
   }
   x = chunk[c0];
-  for (uint32_t w = (c0 / WG + 1) * WG; w < c1; w += WG) {
+  for (uint32_t w = c0 + kMsmFold; w < c1; w += kMsmFold) {
     g2j y = chunk[w];
     jac_add(x, x, y);
   }
@@ -332,11 +335,10 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.tree = p.c == 13;
   p.extra = p.tree ? (uint32_t)p.W : ((uint32_t)p.W << (p.c - 1));
   p.nb = nseg * ((uint32_t)p.W << (p.c - 1));
-  // chunks of <= K points (GBLS_MSM_K; measured r05: K = 8 fills the chip with ~1700 waves but
-  // VALU busy stays at 0.43 -- the chunk loop waits on its point loads, not on SIMDs -- and the
-  // larger folds cost 2.4 % of C2; K = 4 costs 5 %: K = 16 stays)
+  // chunks of <= K points (GBLS_MSM_K), fold groups of kMsmFold chunk partials
   p.K = g_msm_k;
   p.max_chunks = (uint32_t)(((uint64_t)p.W * n + p.K - 1) / p.K) + p.nb;
+  p.max_folds = p.max_chunks / 2 + p.nb;
   size_t o = 0;
   auto take = [&](size_t bytes) {
     size_t at = o;
@@ -347,6 +349,7 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.o_start = take((p.nb + 1) * 4);
   p.o_cur = take(p.nb * 4);
   p.o_cstart = take((p.nb + 1) * 4);
+  for (int l = 0; l < kMsmFoldLevels; l++) p.o_fstart[l] = take((p.nb + 1) * 4);
   p.o_list = take((size_t)p.W * n * 4);
   p.o_chunk = take((size_t)p.max_chunks * sizeof(g2j));
   const size_t tn = p.tree ? p.nb : 0;
@@ -366,17 +369,23 @@ void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
   uint32_t *start = reinterpret_cast<uint32_t *>(ws + p.o_start);
   uint32_t *cur = reinterpret_cast<uint32_t *>(ws + p.o_cur);
   uint32_t *cstart = reinterpret_cast<uint32_t *>(ws + p.o_cstart);
+  MsmFoldStarts fs;
+  for (int l = 0; l < kMsmFoldLevels; l++) fs.l[l] = reinterpret_cast<uint32_t *>(ws + p.o_fstart[l]);
   uint32_t *list = reinterpret_cast<uint32_t *>(ws + p.o_list);
   g2j *chunk = reinterpret_cast<g2j *>(ws + p.o_chunk);
   (void)hipMemsetAsync(cnt, 0, p.nb * 4, st);
   (void)hipMemsetAsync(seg_err, 0, p.nseg * 4, st);
   k_msm_count<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, pks, pre,
                                             pre2, cnt, seg_err);
-  k_msm_scan<<<1, 1024, 0, st>>>(cnt, p.nb, p.K, start, cur, cstart);
+  k_msm_scan<<<1, 1024, 0, st>>>(cnt, p.nb, p.K, start, cur, cstart, fs);
   k_msm_scatter<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, cur,
                                               list);
   k_msm_chunk<<<nblk(p.max_chunks), WG, 0, st>>>(sigs, list, start, cstart, p.nb, p.max_chunks,
                                                  p.K, chunk);
+  for (int l = 0; l < kMsmFoldLevels; l++) {
+    const uint32_t mp = (p.max_folds >> l) + p.nb;
+    k_msm_fold<<<nblk(mp), WG, 0, st>>>(cstart, fs.l[l], p.nb, mp, l, chunk);
+  }
   if (!p.tree) {
     k_msm_pairs<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, p.extra, n, seg_off,
                                            empty_is_error, P, H, seg_err);
