@@ -94,17 +94,19 @@ def cpu_threads():
 
 
 def pmc_traffic(kernel, default_cmd):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
-    summary of the default command without the one-batch leg (profiles/r04/z_c2_pmc_bytes.csv,
-    tools/prof/pmc_bytes.py, from `bench.py --no-single`: 16-batch launches only;
-    FETCH_SIZE doubled per the gfx950 correction).  None for other commands or if absent."""
-    path = os.path.join(ROOT, "profiles", "r04", "z_c2_pmc_bytes.csv")
+    """HBM bytes per launch of `kernel` (a stage name: k_ml_group is the radix-2^28
+    k_ml_group28 of the default build) from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
+    summary of the default command's 16-batch launches (profiles/r05/z_c2_pmc_bytes.csv,
+    tools/prof/pmc_bytes.py --largest; FETCH_SIZE doubled per the gfx950 correction).  None for
+    other commands or if absent."""
+    path = os.path.join(ROOT, "profiles", "r05", "z_c2_pmc_bytes.csv")
     if not default_cmd or not os.path.exists(path):
         return None
     with open(path) as f:
         for row in f.read().splitlines()[1:]:
             cols = row.split(",")
-            if cols[0].split("::")[-1] == kernel:
+            name = cols[0].split("::")[-1].split("<")[0]
+            if name in (kernel, kernel + "28"):
                 return float(cols[4])
     return None
 

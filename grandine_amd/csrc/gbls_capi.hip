@@ -141,6 +141,8 @@ struct Ctx {
   // normal-class streams kept off the CUs reserved for block import while a block is being
   // verified (created on first use, see Engine::block_reserve)
   hipStream_t own_g = nullptr, side1_g = nullptr, side2_g = nullptr;
+  const uint32_t *line_col = nullptr;  // the last pipeline's line columns (LineCols), in tab
+  uint32_t line_ncol = 0;
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
              ev_done = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool done_pending = false;
@@ -536,6 +538,11 @@ struct MlTables {
   };
   size_t plist_off = 0, grp_off = 0, ngroup = 0, v0_n = 1, v1_n = 1;
   std::vector<Level> levels;
+  // the lines' column table (col_off: npairs entries, col[pair] = j ngp + g for pair j of group
+  // g), ngp = groups rounded up to a wave, ncol = ngp x the largest group; ngp = 0: the lines
+  // stay pair-indexed (col_off unset, ncol = npairs)
+  size_t col_off = 0;
+  uint32_t ngp = 0, ncol = 0;
 };
 // count(s): pairs of Miller segment s (>= 1); emit(s, tab): appends their pair indices.
 // npairs: pairs listed; EC: events per launch (line slices).
@@ -606,6 +613,37 @@ MlTables ml_tables(std::vector<uint32_t> &tab, size_t nms, size_t npairs, int EC
   mt.v0_n = mt.ngroup;
   for (size_t l = 0; l < mt.levels.size(); l++)
     (l & 1 ? mt.v0_n : mt.v1_n) = std::max(l & 1 ? mt.v0_n : mt.v1_n, mt.levels[l].nout);
+  // line columns: pair j of group g at j ngp + g, so that a wave of k_ml_group (64 consecutive
+  // groups from a multiple of 64) reads 64 consecutive, 256-byte-aligned words per load
+  uint32_t gmax = 0;
+  for (size_t q = 0; q < mt.ngroup; q++) gmax = std::max(gmax, tab[mt.grp_off + 3 * q + 2]);
+  const uint32_t ngp = (uint32_t)((mt.ngroup + WG - 1) / WG * WG);
+  mt.ncol = (uint32_t)npairs;
+  if (mt.ngroup && (uint64_t)gmax * ngp < (1ull << 32)) {
+    const size_t off = tab.size();
+    tab.resize(off + npairs, 0xffffffffu);
+    bool ok = true;
+    for (size_t q = 0; q < mt.ngroup && ok; q++) {
+      const uint32_t a = tab[mt.grp_off + 3 * q], st = tab[mt.grp_off + 3 * q + 1],
+                     c = tab[mt.grp_off + 3 * q + 2];
+      for (uint32_t j = 0; j < c; j++) {
+        const uint32_t pair = tab[mt.plist_off + a + (size_t)j * st];
+        if (pair >= npairs || tab[off + pair] != 0xffffffffu) {
+          ok = false;
+          break;
+        }
+        tab[off + pair] = j * ngp + (uint32_t)q;
+      }
+    }
+    for (size_t p = 0; ok && p < npairs; p++) ok = tab[off + p] != 0xffffffffu;
+    if (ok) {  // every pair listed exactly once
+      mt.col_off = off;
+      mt.ngp = ngp;
+      mt.ncol = gmax * ngp;
+    } else {
+      tab.resize(off);
+    }
+  }
   return mt;
 }
 
@@ -695,7 +733,6 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   if (event_bytes * ML_EVENTS > g.line_budget)
     EC = (int)std::max<size_t>(1, g.line_budget / event_bytes);
   const bool sliced = EC < ML_EVENTS;
-  const size_t line_words = (size_t)np * EC * 72;
   // Miller segments: the verification segments, or (grouped single checks, grp > 1) runs of
   // grp checks whose pairs (i, n + i) share one Miller product and one final exponentiation
   const bool grouped = grp > 1 && single && !sliced && grp_r;
@@ -721,6 +758,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
           for (uint32_t i = seg_off[s]; i < seg_off[s + 1]; i++) t.push_back(i);
           for (size_t k = 0; k < X; k++) t.push_back((uint32_t)(n + s * X + k));
         });
+  const size_t line_words = (size_t)mt.ncol * EC * 72;
   const size_t chunk_off = tab.size();
   const uint32_t CH = WGR;  // sets per level-1 G2-sum workgroup
   std::vector<uint32_t> seg_chunk(nseg + 1, 0);
@@ -767,6 +805,9 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     sj = c.Sj.as<g2j>();
   }
   const uint32_t *T = c.tab.as<uint32_t>();
+  const LineCols lc{mt.ngp ? T + mt.col_off : nullptr, mt.ncol};
+  c.line_col = lc.col;  // for a grouped re-check of the same lines (grouped_verdicts)
+  c.line_ncol = lc.ncol;
   g2j *gpart = c.gpart.as<g2j>();
   int32_t *gpart_err = reinterpret_cast<int32_t *>(gpart + nchunks);
   // ---- fork
@@ -831,8 +872,8 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   }
   {  // the extra pairs' lines of the first event slice (all events when not sliced)
     StageTimer t(S_LINES_S, side2);
-    if (!sj || !launch_lines_jac(side2, sj, 1, N, NS, NP, c.lines.as<uint32_t>()))
-      launch_lines(side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), NP, 0, EC, c.Ts.as<g2h>(),
+    if (!sj || !launch_lines_jac(side2, sj, 1, N, NS, lc, c.lines.as<uint32_t>()))
+      launch_lines(side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), lc, 0, EC, c.Ts.as<g2h>(),
                    c.lines.as<uint32_t>());
   }
   // latency regime: H(m) stays Jacobian (over Q[2 i]) and its lines take it projectively,
@@ -845,8 +886,8 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   }
   {  // the sets' lines of the first event slice, before the join
     StageTimer t(S_LINES, st);
-    if (!jac_h || !launch_lines_jac(st, c.Q.as<g2j>(), 2, 0, N, NP, c.lines.as<uint32_t>()))
-      launch_lines(st, c.H.as<g2a>(), 0, N, NP, 0, EC, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
+    if (!jac_h || !launch_lines_jac(st, c.Q.as<g2j>(), 2, 0, N, lc, c.lines.as<uint32_t>()))
+      launch_lines(st, c.H.as<g2a>(), 0, N, lc, 0, EC, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
   }
   HIPCHK(hipEventRecord(c.ev_side1, side1));
   HIPCHK(hipEventRecord(c.ev_side2, side2));
@@ -856,10 +897,10 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     const int e1 = std::min(ML_EVENTS, e0 + EC);
     if (e0 > 0) {  // later slices: every pair, after the join
       StageTimer t(S_LINES, st);
-      launch_lines(st, c.H.as<g2a>(), 0, NP, NP, e0, e1, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
+      launch_lines(st, c.H.as<g2a>(), 0, NP, lc, e0, e1, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
     }
     StageTimer t(S_ML_LEAF, st);
-    launch_ml_group(st, c.lines.as<uint32_t>(), NP, c.P.as<g1s>(), T + mt.plist_off,
+    launch_ml_group(st, c.lines.as<uint32_t>(), lc, mt.ngp, c.P.as<g1s>(), T + mt.plist_off,
                     T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>(), c.V28.as<uint32_t>());
   }
   ml_tail(c, st, mt, T, (uint32_t)nms, partials, n <= kSplitHornerMaxSets);
@@ -958,7 +999,8 @@ bool grouped_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *ms
     launch_redo_tables(st, redo, cnt, base, (uint32_t)R, (uint32_t)n, plist, grp);
     {
       StageTimer t(S_ML_LEAF, st);
-      launch_ml_group(st, c.lines.as<uint32_t>(), (uint32_t)(2 * n), c.P.as<g1s>(), plist, grp, (uint32_t)R, 0,
+      launch_ml_group(st, c.lines.as<uint32_t>(), LineCols{c.line_col, c.line_ncol}, 0, c.P.as<g1s>(), plist, grp,
+                      (uint32_t)R, 0,
                       ML_EVENTS, c.V0.as<fp12>(), c.V28.as<uint32_t>());
     }
     {

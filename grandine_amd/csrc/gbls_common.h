@@ -131,19 +131,26 @@ void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
                 int32_t *seg_err);
 
 // k_lines.hip -- Miller-loop line functions of every pair
-// lines of events [e0, e1) of pairs [first, first + count) of np (H indexed by pair),
-// stored at event e - e0; Ts: the running point between event slices (null: full range)
-void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
+// Where a pair's lines live: column col[pair] of ncol (col null: column = pair); word w of
+// event e at (e * 72 + w) * ncol + column (bls_pairing.h line_word)
+struct LineCols {
+  const uint32_t *col;
+  uint32_t ncol;
+};
+// lines of events [e0, e1) of pairs [first, first + count) (H indexed by pair), stored at
+// event e - e0; Ts: the running point between event slices (null: full range)
+void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, LineCols lc,
                   int e0, int e1, g2h *Ts, uint32_t *lines);
 // all events of pairs [first, first + count) from Jacobian points Qj[stride i] (count <=
 // kW4Max, else false)
 bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t first, uint32_t count,
-                      uint32_t np, uint32_t *lines);
+                      LineCols lc, uint32_t *lines);
 
 // k_miller.hip -- Miller product tree + Horner
 // groups: (first index into plist, stride, count) per group, segment by segment
-// events [e0, e1): lines at event e - e0, products to V0[e * ngroup + g]
-void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
+// events [e0, e1): lines at event e - e0, products to V0[e * ngroup + g]; the lines of pair j
+// of group g at column j ngp + g when ngp != 0 (the tables' layout), else at lc's column
+void launch_ml_group(hipStream_t st, const uint32_t *lines, LineCols lc, uint32_t ngp, const g1s *P,
                      const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
                      int e1, fp12 *V0, uint32_t *V28);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,

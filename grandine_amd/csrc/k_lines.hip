@@ -1,6 +1,10 @@
 // gfx950 kernel: the 68 Miller-loop line functions (63 doubling + 5 addition steps
 // along |x|) of every pair's G2 point, stored structure-of-arrays (bls_pairing.h
-// line_word) so that each later load is one coalesced dword per lane.  One DPP quad per
+// line_word) so that each later load is one coalesced dword per lane.  A pair's lines go to
+// its COLUMN (LineCols: col[pair], or the pair itself): the Miller-product tables place pair
+// j of group g at column j ngp + g (ngp = groups rounded up to 64), so that every wave of
+// k_ml_group reads 64 consecutive, 256-byte-aligned words per load (r05: the pair-indexed
+// layout straddled three 128-B lines per wave load, 1.38x the line bytes in FETCH_SIZE).  One DPP quad per
 // pair: doubling and addition steps run quad-cooperatively (bls_gang.h gang_line_dbl,
 // gang_line_add_aff); lane q stores line components c with c % 4 == q.  Large batches
 // generate and consume the lines in event slices (the running point T kept in HBM
@@ -38,19 +42,20 @@ __device__ __forceinline__ void line_put_row(uint32_t *L, uint32_t np, uint32_t 
 
 // lines_range (bls_pairing.h) with quad doubling and addition steps: events [e0, e1)
 __global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t first, uint32_t count,
-                                              uint32_t np, int e0, int e1, g2h *Ts, uint32_t *L) {
+                                              LineCols lc, int e0, int e1, g2h *Ts, uint32_t *L) {
   uint32_t t = blockIdx.x * WG + threadIdx.x;
   uint32_t i = t >> 2;
   int q = (int)(t & 3);
   if (i >= count) return;  // whole quads only
   uint32_t pair = first + i;
+  const uint32_t np = lc.ncol, cp = lc.col ? lc.col[pair] : pair;  // the line column
   g2a Q = H[pair];
   fp2 L0, L2, L3;
   if (aff_is_inf(Q)) {
     fp2_one(L0);
     fp2_zero(L2);
     fp2_zero(L3);
-    for (int e = e0; e < e1; e++) line_put_q(L, np, pair, e - e0, q, L0, L2, L3);
+    for (int e = e0; e < e1; e++) line_put_q(L, np, cp, e - e0, q, L0, L2, L3);
     return;
   }
   g2h T;
@@ -66,27 +71,28 @@ __global__ void __launch_bounds__(WG) k_lines(const g2a *H, uint32_t first, uint
       gang_line_dbl(T, L0, L2, L3, q);
     else
       gang_line_add_aff(T, Q, L0, L2, L3, q);
-    line_put_q(L, np, pair, e - e0, q, L0, L2, L3);
+    line_put_q(L, np, cp, e - e0, q, L0, L2, L3);
   }
   if (e1 < ML_EVENTS && q == 0) Ts[pair] = T;
 }
 
 // the same on a 16-lane row (small launches); lanes 0-5 store one component each
 __global__ void __launch_bounds__(WG) k_lines_row(const g2a *H, uint32_t first, uint32_t count,
-                                                  uint32_t np, int e0, int e1, g2h *Ts,
+                                                  LineCols lc, int e0, int e1, g2h *Ts,
                                                   uint32_t *L) {
   uint32_t t = blockIdx.x * WG + threadIdx.x;
   uint32_t i = t >> 4;
   int l = (int)(t & 15);
   if (i >= count) return;  // whole rows
   uint32_t pair = first + i;
+  const uint32_t np = lc.ncol, cp = lc.col ? lc.col[pair] : pair;  // the line column
   g2a Q = H[pair];
   fp2 L0, L2, L3;
   if (aff_is_inf(Q)) {
     fp2_one(L0);
     fp2_zero(L2);
     fp2_zero(L3);
-    for (int e = e0; e < e1; e++) line_put_row(L, np, pair, e - e0, l, L0, L2, L3);
+    for (int e = e0; e < e1; e++) line_put_row(L, np, cp, e - e0, l, L0, L2, L3);
     return;
   }
   g2h T;
@@ -102,7 +108,7 @@ __global__ void __launch_bounds__(WG) k_lines_row(const g2a *H, uint32_t first, 
       row_line_dbl(T, L0, L2, L3, l);
     else
       row_line_add_aff(T, Q, L0, L2, L3, l);
-    line_put_row(L, np, pair, e - e0, l, L0, L2, L3);
+    line_put_row(L, np, cp, e - e0, l, L0, L2, L3);
   }
   if (e1 < ML_EVENTS && l == 0) Ts[pair] = T;
 }
@@ -185,14 +191,15 @@ __device__ __forceinline__ void lane_line_add_aff(g2h &T, const g2a &Q, uint32_t
 // one lane per pair (serial lines_range): a quarter of the quad's instructions per pair,
 // for launches that fill the chip on their own
 __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first, uint32_t count,
-                                                   uint32_t np, int e0, int e1, g2h *Ts,
+                                                   LineCols lc, int e0, int e1, g2h *Ts,
                                                    uint32_t *L) {
   uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= count) return;
   const uint32_t pair = first + i;
+  const uint32_t np = lc.ncol, cp = lc.col ? lc.col[pair] : pair;  // the line column
   const g2a Q = H[pair];
   if (aff_is_inf(Q)) {
-    lines_range(L, np, pair, Q, e0, e1, Ts);  // identity lines
+    lines_range(L, np, cp, Q, e0, e1, Ts);  // identity lines
     return;
   }
   g2h T;
@@ -205,9 +212,9 @@ __global__ void __launch_bounds__(WG) k_lines_lane(const g2a *H, uint32_t first,
   }
   for (int e = e0; e < e1; e++) {
     if (ev_is_dbl(e))
-      lane_line_dbl(T, L, np, pair, e - e0);
+      lane_line_dbl(T, L, np, cp, e - e0);
     else
-      lane_line_add_aff(T, Q, L, np, pair, e - e0);
+      lane_line_add_aff(T, Q, L, np, cp, e - e0);
   }
   if (e1 < ML_EVENTS) Ts[pair] = T;
 }
@@ -229,13 +236,14 @@ __device__ __forceinline__ void put28(uint32_t *L, uint32_t np, uint32_t pair, i
   for (int i = 0; i < 12; i++) L[line_word(e, c + 1, i, np, pair)] = w.l[i];
 }
 __global__ void __launch_bounds__(WG) k_lines_lane28(const g2a *H, uint32_t first, uint32_t count,
-                                                     uint32_t np, int e0, int e1, g2h *Ts, uint32_t *L) {
+                                                     LineCols lc, int e0, int e1, g2h *Ts, uint32_t *L) {
   uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= count) return;
   const uint32_t pair = first + i;
+  const uint32_t np = lc.ncol, cp = lc.col ? lc.col[pair] : pair;  // the line column
   const g2a Q = H[pair];
   if (aff_is_inf(Q)) {
-    lines_range(L, np, pair, Q, e0, e1, Ts);  // identity lines (engine form)
+    lines_range(L, np, cp, Q, e0, e1, Ts);  // identity lines (engine form)
     return;
   }
   __shared__ r28::fe2 qs[2 * WG];
@@ -257,7 +265,7 @@ __global__ void __launch_bounds__(WG) k_lines_lane28(const g2a *H, uint32_t firs
   }
   for (int e = e0; e < e1; e++) {
     const int el = e - e0;
-    auto put = [&](int c, const r28::fe2 &v) { put28(L, np, pair, el, c, v); };
+    auto put = [&](int c, const r28::fe2 &v) { put28(L, np, cp, el, c, v); };
     if (ev_is_dbl(e))
       r28::line_dbl28(T, put);
     else
@@ -285,11 +293,12 @@ __device__ __forceinline__ void line_put_w4(const w4::Ctx &c, uint32_t *L, uint3
 }
 template <bool X>
 __global__ void __launch_bounds__(64) k_lines_w4(const g2a *H, uint32_t first, uint32_t count,
-                                                 uint32_t np, int e0, int e1, g2h *Ts, uint32_t *L) {
+                                                 LineCols lc, int e0, int e1, g2h *Ts, uint32_t *L) {
   if constexpr (X) w4::exclusive_simd();
   const uint32_t i = blockIdx.x;
   if (i >= count) return;  // whole waves
   const uint32_t pair = first + i;
+  const uint32_t np = lc.ncol, cp = lc.col ? lc.col[pair] : pair;  // the line column
   const g2a Q = H[pair];
   const uint32_t j = threadIdx.x & 15, r = (threadIdx.x >> 4) & 3;
   if (aff_is_inf(Q)) {  // identity lines: L0 = 1, L2 = L3 = 0
@@ -298,7 +307,7 @@ __global__ void __launch_bounds__(64) k_lines_w4(const g2a *H, uint32_t first, u
     for (int k = 0; k < 12; k++) one = j == (uint32_t)k ? k::ONE_M[k] : one;
     for (int e = e0; e < e1; e++)
       for (uint32_t cc = r; cc < 6; cc += 4)
-        if (j < 12) L[line_word(e - e0, (int)cc, (int)j, np, pair)] = cc == 0 ? one : 0u;
+        if (j < 12) L[line_word(e - e0, (int)cc, (int)j, np, cp)] = cc == 0 ? one : 0u;
     return;
   }
   w4::Ctx c;
@@ -323,7 +332,7 @@ __global__ void __launch_bounds__(64) k_lines_w4(const g2a *H, uint32_t first, u
       w4::line_dbl(c, T, l0, l2, l3);
     else
       w4::line_add_aff(c, T, q, l0, l2, l3);
-    line_put_w4(c, L, np, pair, e - e0, l0, l2, l3);
+    line_put_w4(c, L, np, cp, e - e0, l0, l2, l3);
   }
   if (e1 < ML_EVENTS) {
     g2h *o = Ts + pair;
@@ -339,10 +348,11 @@ __global__ void __launch_bounds__(64) k_lines_w4(const g2a *H, uint32_t first, u
 // scaled by Fp2 factors, which the final exponentiation removes)
 template <bool X>
 __global__ void __launch_bounds__(64) k_lines_w4j(const g2j *Qj, uint32_t stride, uint32_t first,
-                                                  uint32_t count, uint32_t np, uint32_t *L) {
+                                                  uint32_t count, LineCols lc, uint32_t *L) {
   if constexpr (X) w4::exclusive_simd();
   const uint32_t i = blockIdx.x, pair = first + i;
   if (i >= count) return;  // whole waves
+  const uint32_t np = lc.ncol, cp = lc.col ? lc.col[pair] : pair;  // the line column
   const uint32_t j = threadIdx.x & 15, r = (threadIdx.x >> 4) & 3;
   w4::Ctx c;
   w4::init(c);
@@ -354,7 +364,7 @@ __global__ void __launch_bounds__(64) k_lines_w4j(const g2j *Qj, uint32_t stride
     for (int k = 0; k < 12; k++) one = j == (uint32_t)k ? k::ONE_M[k] : one;
     for (int e = 0; e < ML_EVENTS; e++)
       for (uint32_t cc = r; cc < 6; cc += 4)
-        if (j < 12) L[line_word(e, (int)cc, (int)j, np, pair)] = cc == 0 ? one : 0u;
+        if (j < 12) L[line_word(e, (int)cc, (int)j, np, cp)] = cc == 0 ? one : 0u;
     return;
   }
   w4::jac_to_hom(c, q, q);
@@ -365,31 +375,31 @@ __global__ void __launch_bounds__(64) k_lines_w4j(const g2j *Qj, uint32_t stride
       w4::line_dbl(c, T, l0, l2, l3);
     else
       w4::line_add_proj(c, T, q, l0, l2, l3);
-    line_put_w4(c, L, np, pair, e, l0, l2, l3);
+    line_put_w4(c, L, np, cp, e, l0, l2, l3);
   }
 }
 bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t first, uint32_t count,
-                      uint32_t np, uint32_t *lines) {
+                      LineCols lc, uint32_t *lines) {
   if (!count || count > kW4Max) return false;
   (count <= w4::kExclusiveMaxWaves ? k_lines_w4j<true> : k_lines_w4j<false>)<<<count, 64, 0, st>>>(
-      Qj, stride, first, count, np, lines);
+      Qj, stride, first, count, lc, lines);
   return true;
 }
 
-void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, uint32_t np,
+void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, LineCols lc,
                   int e0, int e1, g2h *Ts, uint32_t *lines) {
   if (!count) return;
   if (count <= kW4Max)
     (count <= w4::kExclusiveMaxWaves ? k_lines_w4<true> : k_lines_w4<false>)<<<count, 64, 0, st>>>(
-        H, first, count, np, e0, e1, Ts, lines);
+        H, first, count, lc, e0, e1, Ts, lines);
   else if (count >= kLaneRegimeLines && g_lane_r28)
-    k_lines_lane28<<<nblk(count), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
+    k_lines_lane28<<<nblk(count), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);
   else if (count >= kLaneRegimeLines)
-    k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
+    k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);
   else if (count <= kRowRegimeMax)
-    k_lines_row<<<nblk((size_t)count * 16), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
+    k_lines_row<<<nblk((size_t)count * 16), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);
   else
-    k_lines<<<nblk((size_t)count * 4), WG, 0, st>>>(H, first, count, np, e0, e1, Ts, lines);
+    k_lines<<<nblk((size_t)count * 4), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);
 }
 
 }  // namespace gbls

@@ -16,10 +16,15 @@
 
 namespace gbls {
 
-__device__ __forceinline__ void ml_eval(sp034 &s, const uint32_t *L, uint32_t np, const g1s *P,
-                                        uint32_t pair, int e) {
+// the line column of pair j of group g (pair id `pair`): the tables' layout j ngp + g, or lc's
+__device__ __forceinline__ uint32_t ml_col(const LineCols &lc, uint32_t ngp, uint32_t g, uint32_t j,
+                                           uint32_t pair) {
+  return ngp ? j * ngp + g : (lc.col ? lc.col[pair] : pair);
+}
+__device__ __forceinline__ void ml_eval(sp034 &s, const uint32_t *L, uint32_t ncol, uint32_t col,
+                                        const g1s *P, uint32_t pair, int e) {
   fp2 L0, L2, L3;
-  line_get(L, np, pair, e, L0, L2, L3);
+  line_get(L, ncol, col, e, L0, L2, L3);
   g1s Pp = P[pair];
   line_eval_s(s, L0, L2, L3, Pp);
 }
@@ -35,7 +40,7 @@ __device__ __forceinline__ uint32_t xcd_work_index(uint32_t b, uint32_t nwg) {
   const uint32_t xcd = b % 8, q = nwg / 8, r = nwg % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
-__global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np, const g1s *P,
+__global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, LineCols lc, uint32_t ngp, const g1s *P,
                                                  const uint32_t *plist, const uint32_t *grp,
                                                  uint32_t ngroup, int e0, int ne, int xcd_order,
                                                  fp12 *V0) {
@@ -54,16 +59,21 @@ __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np,
   int e = e0 + el;
   if (g >= ngroup) return;
   uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
+  const uint32_t nc = lc.ncol;
+  auto eval = [&](sp034 &sx, uint32_t j) {
+    const uint32_t pair = plist[at + j * stride];
+    ml_eval(sx, L, nc, ml_col(lc, ngp, g, j, pair), P, pair, el);
+  };
   sp034 sa, sb;
   fp12 acc;
-  ml_eval(sa, L, np, P, plist[at], el);
+  eval(sa, 0);
   if (cnt == 1) {
     sp_to_fp12(acc, sa);
   } else {
-    ml_eval(sb, L, np, P, plist[at + stride], el);
+    eval(sb, 1);
     sp_mul_sp(acc, sa, sb);
     for (uint32_t j = 2; j < cnt; j++) {
-      ml_eval(sa, L, np, P, plist[at + j * stride], el);
+      eval(sa, j);
       fp12_mul_034(acc, acc, sa);
     }
   }
@@ -82,8 +92,8 @@ __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, uint32_t np,
 // the line of event e at pair `pair`, evaluated at its G1 point, in radix 2^28: one line
 // component (12 engine words) at a time, the next one's loads in flight during this one's
 // product, so at most two components and the point's current coordinate are live
-__device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_t np, const g1s *P,
-                                          uint32_t pair, int e) {
+__device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_t np, uint32_t col,
+                                          const g1s *P, uint32_t pair, int e) {
   const g1s *Pp = P + pair;
   fp pc;
 #pragma unroll
@@ -95,7 +105,7 @@ __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_
   r28::fe *out[6] = {&s.a0.c0, &s.a0.c1, &s.a2.c0, &s.a2.c1, &s.a3.c0, &s.a3.c1};
   uint32_t cur[12], nxt[12];
 #pragma unroll
-  for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, 0, i, np, pair)];
+  for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, 0, i, np, col)];
   r28::fe q;
   r28::repack_in(q, pc);
 #pragma unroll
@@ -104,7 +114,7 @@ __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_
     for (int i = 0; i < 12; i++) cur[i] = nxt[i];
     if (c < 5) {
 #pragma unroll
-      for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, c + 1, i, np, pair)];
+      for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, c + 1, i, np, col)];
     }
     if (c == 2 || c == 4) {  // the point's x for L2, its y for L3
       fp t;
@@ -127,10 +137,10 @@ typedef const void __attribute__((address_space(1))) *gptr_t;
 typedef void __attribute__((address_space(3))) *lptr_t;
 // LDS staging of the line (g_ml_dma, the default): the 72 line words of one pair's event into the wave's LDS stage (word w of lane l at
 // lbuf[w * WG + l]): global -> LDS DMA loads, no VGPR destination, one coalesced dword per lane
-__device__ __forceinline__ void ml_stage28(uint32_t *lbuf, const uint32_t *L, uint32_t np, uint32_t pair, int e) {
+__device__ __forceinline__ void ml_stage28(uint32_t *lbuf, const uint32_t *L, uint32_t np, uint32_t col, int e) {
 #pragma unroll
   for (int w = 0; w < 72; w++)
-    __builtin_amdgcn_global_load_lds((gptr_t)(L + line_word(e, w / 12, w % 12, np, pair)),
+    __builtin_amdgcn_global_load_lds((gptr_t)(L + line_word(e, w / 12, w % 12, np, col)),
                                      (lptr_t)(lbuf + w * WG), 4, 0, 0);
 }
 // the staged line evaluated at the pair's G1 point (loaded one pair ahead, ml_p_load), from
@@ -176,7 +186,7 @@ __device__ __forceinline__ void dma_wait() {
 __device__ __forceinline__ void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 template <bool DMA>
-__global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t np, const g1s *P,
+__global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, LineCols lc, uint32_t ngp, const g1s *P,
                                                    const uint32_t *plist, const uint32_t *grp,
                                                    uint32_t ngroup, int e0, int ne, int xcd_order,
                                                    uint32_t *V28) {
@@ -196,6 +206,8 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
   if (g >= ngroup) return;
   uint32_t at = grp[3 * g], stride = grp[3 * g + 1], cnt = grp[3 * g + 2];
   __shared__ uint32_t park[84 * WG];
+  const uint32_t np = lc.ncol;
+  auto colj = [&](uint32_t j, uint32_t pair) { return ml_col(lc, ngp, g, j, pair); };
   r28::sp sa, sb;
   r28::fe12 acc;
   if constexpr (DMA) {
@@ -209,7 +221,7 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
     // (a loop-carried index load was waited at once: its VGPR -> AGPR copy)
     MlP pp;
     uint32_t pn = plist[at];
-    ml_stage28(lbuf, L, np, pn, el);
+    ml_stage28(lbuf, L, np, colj(0, pn), el);
     ml_p_load(pp, P, pn);
     dma_wait();
     pn = plist[at + (cnt > 1 ? stride : 0)];  // unconditional: a phi would wait on the load
@@ -218,14 +230,14 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
     if (cnt == 1) {
       r28::sp_to_fe12(acc, sa);
     } else {
-      ml_stage28(lbuf, L, np, pn, el);
+      ml_stage28(lbuf, L, np, colj(1, pn), el);
       ml_p_load(pp, P, pn);
       dma_wait();
       pn = plist[at + (cnt > 2 ? 2 * stride : 0)];
       ml_eval28_lds(sb, lb, pp);
       lds_reads_done();
       if (cnt > 2) {
-        ml_stage28(lbuf, L, np, pn, el);
+        ml_stage28(lbuf, L, np, colj(2, pn), el);
         ml_p_load(pp, P, pn);
       }
       r28::sp_mul_sp_lazy(acc, sa, sb);
@@ -235,21 +247,25 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, uint32_t n
         ml_eval28_lds(sa, lb, pp);
         lds_reads_done();
         if (j + 1 < cnt) {
-          ml_stage28(lbuf, L, np, pn, el);
+          ml_stage28(lbuf, L, np, colj(j + 1, pn), el);
           ml_p_load(pp, P, pn);
         }
         r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
       }
     }
   } else {
-    ml_eval28(sa, L, np, P, plist[at], el);
+    auto eval = [&](r28::sp &sx, uint32_t j) {
+      const uint32_t pair = plist[at + j * stride];
+      ml_eval28(sx, L, np, colj(j, pair), P, pair, el);
+    };
+    eval(sa, 0);
     if (cnt == 1) {
       r28::sp_to_fe12(acc, sa);
     } else {
-      ml_eval28(sb, L, np, P, plist[at + stride], el);
+      eval(sb, 1);
       r28::sp_mul_sp_lazy(acc, sa, sb);
       for (uint32_t j = 2; j < cnt; j++) {
-        ml_eval28(sa, L, np, P, plist[at + j * stride], el);
+        eval(sa, j);
         r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
       }
     }
@@ -330,7 +346,7 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
   w12_store(partial + s, acc);
 }
 
-void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g1s *P,
+void launch_ml_group(hipStream_t st, const uint32_t *lines, LineCols lc, uint32_t ngp, const g1s *P,
                      const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
                      int e1, fp12 *V0, uint32_t *V28) {
   dim3 grid(nblk(ngroup), e1 - e0);
@@ -338,14 +354,14 @@ void launch_ml_group(hipStream_t st, const uint32_t *lines, uint32_t np, const g
   const dim3 grid1(nblk(ngroup) * (uint32_t)(e1 - e0));
   if (g_ml_r28 && V28) {
     if (g_ml_dma)
-      k_ml_group28<true><<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+      k_ml_group28<true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     else
-      k_ml_group28<false><<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+      k_ml_group28<false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     const uint32_t nvals = ngroup * (uint32_t)(e1 - e0);
     k_ml_pack28<<<nblk((size_t)nvals * 12), WG, 0, st>>>(V28, ngroup, e0, nvals, V0);
     return;
   }
-  k_ml_group<<<grid1, WG, 0, st>>>(lines, np, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V0);
+  k_ml_group<<<grid1, WG, 0, st>>>(lines, lc, ngp, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V0);
 }
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout) {
