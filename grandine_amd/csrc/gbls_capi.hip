@@ -48,6 +48,7 @@ uint32_t gbls::g_ml_r28 = 1;
 uint32_t gbls::g_msm_k = gbls::kMsmChunk;
 uint32_t gbls::g_ml_xcd = 1;
 uint32_t gbls::g_ml_dma = 0;
+uint32_t gbls::g_ml_prefetch = 1;
 uint32_t gbls::g_lane_r28 = 1;
 
 namespace {
@@ -156,7 +157,7 @@ struct Ctx {
   hipStream_t cur = nullptr;          // its main stream (nullptr = the legacy default stream)
   bool used = false;                  // last_stream is meaningful
   hipStream_t last_stream = nullptr;  // main stream of the previous call
-  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, R, Sj, gpart, lines, Ts, V0, V1, V28, hparts, tab, part, err, out0,
+  Buf in0, in1, in2, in3, in4, in5, U, Q, H, P, Pc, R, Sj, gpart, lines, Ts, V0, V1, V28, hparts, tab, part, err, out0,
       out1, pks, pre, pre2, msm, sigd, sigst, rnd, ng1, gerr, gv, redo, rtab;
   // per-call option of the next pipeline_partials on this lease: compressed signatures
   // (96 B each, device) to decompress on the signature-side stream into `sigs`, with their
@@ -432,6 +433,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_BLOCK_HOLD")) g.block_hold = std::atoi(e) != 0;
     if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_ML_DMA")) g_ml_dma = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_ML_PREFETCH")) g_ml_prefetch = (uint32_t)std::strtoul(e, nullptr, 10);
   }
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
@@ -793,6 +795,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
       !c.ensure(c.V0, ML_EVENTS * mt.v0_n * sizeof(fp12)) ||
       !c.ensure(c.V1, ML_EVENTS * mt.v1_n * sizeof(fp12)) ||
       (g_ml_r28 && !c.ensure(c.V28, (size_t)ML_EVENTS * 168 * 4 * mt.ngroup)) ||
+      (g_ml_r28 && mt.ngp && !c.ensure(c.Pc, (size_t)36 * 4 * mt.ncol)) ||
       !c.ensure(c.hparts, 4 * 64 * sizeof(fp12)))  // the split Horner's parts (<= 64 segments)
     return false;
   if (!c.upload_staged(c.tab, tab.data(), tab.size() * 4, st)) return false;
@@ -893,6 +896,11 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   HIPCHK(hipEventRecord(c.ev_side2, side2));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side1, 0));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
+  const uint32_t *Pc = nullptr;  // the points by line column (radix-2^28 Miller kernel)
+  if (g_ml_r28 && mt.ngp) {
+    launch_ml_pcols(st, c.P.as<g1s>(), lc.col, NP, lc.ncol, c.Pc.as<uint32_t>());
+    Pc = c.Pc.as<uint32_t>();
+  }
   for (int e0 = 0; e0 < ML_EVENTS; e0 += EC) {
     const int e1 = std::min(ML_EVENTS, e0 + EC);
     if (e0 > 0) {  // later slices: every pair, after the join
@@ -900,7 +908,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
       launch_lines(st, c.H.as<g2a>(), 0, NP, lc, e0, e1, c.Ts.as<g2h>(), c.lines.as<uint32_t>());
     }
     StageTimer t(S_ML_LEAF, st);
-    launch_ml_group(st, c.lines.as<uint32_t>(), lc, mt.ngp, c.P.as<g1s>(), T + mt.plist_off,
+    launch_ml_group(st, c.lines.as<uint32_t>(), lc, mt.ngp, c.P.as<g1s>(), Pc, T + mt.plist_off,
                     T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>(), c.V28.as<uint32_t>());
   }
   ml_tail(c, st, mt, T, (uint32_t)nms, partials, n <= kSplitHornerMaxSets);
@@ -999,7 +1007,8 @@ bool grouped_verdicts(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *ms
     launch_redo_tables(st, redo, cnt, base, (uint32_t)R, (uint32_t)n, plist, grp);
     {
       StageTimer t(S_ML_LEAF, st);
-      launch_ml_group(st, c.lines.as<uint32_t>(), LineCols{c.line_col, c.line_ncol}, 0, c.P.as<g1s>(), plist, grp,
+      launch_ml_group(st, c.lines.as<uint32_t>(), LineCols{c.line_col, c.line_ncol}, 0, c.P.as<g1s>(), nullptr,
+                      plist, grp,
                       (uint32_t)R, 0,
                       ML_EVENTS, c.V0.as<fp12>(), c.V28.as<uint32_t>());
     }

@@ -43,6 +43,7 @@ constexpr uint32_t kMsmChunk = 16;
 constexpr int kMsmFoldLevels = 3;        // k_msm_fold: pairwise levels over each bucket's partials
 constexpr uint32_t kMsmFold = 1u << kMsmFoldLevels;  // chunk partials per fold group
 extern uint32_t g_msm_k;                 // kMsmChunk unless GBLS_MSM_K is set
+extern uint32_t g_ml_prefetch;           // k_ml_group28: next pair's line loaded during the product (GBLS_ML_PREFETCH)
 extern uint32_t g_ml_dma;                // k_ml_group28: line staged in LDS by DMA loads (GBLS_ML_DMA)
 extern uint32_t g_ml_xcd;                // k_ml_group: XCD-grouped block order (GBLS_ML_XCD)
 extern uint32_t g_lane_r28;              // lane-regime clearing / lines in radix 2^28 (GBLS_LANE_R28)
@@ -150,9 +151,13 @@ bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t f
 // groups: (first index into plist, stride, count) per group, segment by segment
 // events [e0, e1): lines at event e - e0, products to V0[e * ngroup + g]; the lines of pair j
 // of group g at column j ngp + g when ngp != 0 (the tables' layout), else at lc's column
+// Pc (nullable): the points by line column (launch_ml_pcols), read by the radix-2^28 kernel
 void launch_ml_group(hipStream_t st, const uint32_t *lines, LineCols lc, uint32_t ngp, const g1s *P,
-                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
-                     int e1, fp12 *V0, uint32_t *V28);
+                     const uint32_t *Pc, const uint32_t *plist, const uint32_t *groups, uint32_t ngroup,
+                     int e0, int e1, fp12 *V0, uint32_t *V28);
+// Pc[w * ncol + col[pair]] = word w of P[pair] (36 words per point), pairs [0, np)
+void launch_ml_pcols(hipStream_t st, const g1s *P, const uint32_t *col, uint32_t np, uint32_t ncol,
+                     uint32_t *Pc);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);
 // lim (device count, optional): only segments s with base + s < *lim run (the others exit)

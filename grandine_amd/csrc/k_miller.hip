@@ -89,15 +89,27 @@ __global__ void __launch_bounds__(WG) k_ml_group(const uint32_t *L, LineCols lc,
 // in-place order parks live in LDS (fe12_mul_034_lazy_st, 84 words per lane), the line is
 // evaluated one component at a time (ml_eval28), and the result leaves as raw radix-2^28
 // words (k_ml_pack28 converts them): 256 VGPRs + ~140 AGPRs, no scratch.
-// the line of event e at pair `pair`, evaluated at its G1 point, in radix 2^28: one line
-// component (12 engine words) at a time, the next one's loads in flight during this one's
-// product, so at most two components and the point's current coordinate are live
-__device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_t np, uint32_t col,
-                                          const g1s *P, uint32_t pair, int e) {
-  const g1s *Pp = P + pair;
-  fp pc;
+// the line of event e at pair `pair` (line column col), evaluated at its G1 point, in radix
+// 2^28: one line component (12 engine words) at a time, the next one's loads in flight during
+// this one's product, so at most two components and the point's current coordinate are live.
+// The point comes from Pc (the points by line column, word w of column c at w * np + c:
+// coalesced, k_ml_pcols) when given, else from P; its x is loaded one component ahead of its
+// use, its y two.
+__device__ __forceinline__ void ml_pword(fp &r, const g1s *P, const uint32_t *Pc, uint32_t np,
+                                         uint32_t col, uint32_t pair, int k) {
+  if (Pc) {
 #pragma unroll
-  for (int i = 0; i < 12; i++) pc.l[i] = Pp->c.l[i];
+    for (int i = 0; i < 12; i++) r.l[i] = Pc[(size_t)(12 * k + i) * np + col];
+  } else {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(P + pair) + 12 * k;
+#pragma unroll
+    for (int i = 0; i < 12; i++) r.l[i] = w[i];
+  }
+}
+__device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_t np, uint32_t col,
+                                          const g1s *P, const uint32_t *Pc, uint32_t pair, int e) {
+  fp pc;
+  ml_pword(pc, P, Pc, np, col, pair, 2);
   if (fp_is_zero(pc)) {
     r28::sp_identity(s);
     return;
@@ -106,6 +118,8 @@ __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_
   uint32_t cur[12], nxt[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, 0, i, np, col)];
+  fp pxy;
+  ml_pword(pxy, P, Pc, np, col, pair, 0);  // x, for L2
   r28::fe q;
   r28::repack_in(q, pc);
 #pragma unroll
@@ -116,17 +130,48 @@ __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_
 #pragma unroll
       for (int i = 0; i < 12; i++) nxt[i] = L[line_word(e, c + 1, i, np, col)];
     }
-    if (c == 2 || c == 4) {  // the point's x for L2, its y for L3
-      fp t;
-      const fp &src = c == 2 ? Pp->x : Pp->y;
-#pragma unroll
-      for (int i = 0; i < 12; i++) t.l[i] = src.l[i];
-      r28::repack_in(q, t);
-    }
+    if (c == 2 || c == 4) r28::repack_in(q, pxy);  // the point's x for L2, its y for L3
+    if (c == 2) ml_pword(pxy, P, Pc, np, col, pair, 1);
     asm volatile("" ::: "memory");
     fp w;
 #pragma unroll
     for (int i = 0; i < 12; i++) w.l[i] = cur[i];
+    r28::fe t;
+    r28::repack_in(t, w);
+    r28::mul(*out[c], t, q);
+    asm volatile("" ::: "memory");
+  }
+}
+// the line words of one pair (72, component-major) loaded as a block: the Miller kernel loads
+// pair j + 1's while pair j's product runs (they wait in AGPRs), so no line load is exposed
+__device__ __forceinline__ void ml_line_load(uint32_t (&lw)[72], const uint32_t *L, uint32_t np,
+                                             uint32_t col, int e) {
+#pragma unroll
+  for (int w = 0; w < 72; w++) lw[w] = L[line_word(e, w / 12, w % 12, np, col)];
+}
+// ml_eval28 on a loaded line
+__device__ __forceinline__ void ml_eval28_reg(r28::sp &s, const uint32_t (&lw)[72], uint32_t np,
+                                              uint32_t col, const g1s *P, const uint32_t *Pc,
+                                              uint32_t pair) {
+  fp pc;
+  ml_pword(pc, P, Pc, np, col, pair, 2);
+  if (fp_is_zero(pc)) {
+    r28::sp_identity(s);
+    return;
+  }
+  r28::fe *out[6] = {&s.a0.c0, &s.a0.c1, &s.a2.c0, &s.a2.c1, &s.a3.c0, &s.a3.c1};
+  fp pxy;
+  ml_pword(pxy, P, Pc, np, col, pair, 0);  // x, for L2
+  r28::fe q;
+  r28::repack_in(q, pc);
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    if (c == 2 || c == 4) r28::repack_in(q, pxy);  // the point's x for L2, its y for L3
+    if (c == 2) ml_pword(pxy, P, Pc, np, col, pair, 1);
+    asm volatile("" ::: "memory");
+    fp w;
+#pragma unroll
+    for (int i = 0; i < 12; i++) w.l[i] = lw[12 * c + i];
     r28::fe t;
     r28::repack_in(t, w);
     r28::mul(*out[c], t, q);
@@ -185,8 +230,9 @@ __device__ __forceinline__ void dma_wait() {
 }
 __device__ __forceinline__ void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <bool DMA>
+template <bool DMA, bool g_prefetch>
 __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, LineCols lc, uint32_t ngp, const g1s *P,
+                                                   const uint32_t *Pc,
                                                    const uint32_t *plist, const uint32_t *grp,
                                                    uint32_t ngroup, int e0, int ne, int xcd_order,
                                                    uint32_t *V28) {
@@ -254,9 +300,25 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, LineCols l
       }
     }
   } else {
+    // pair j + 1's line loaded while pair j's product runs (g_ml_prefetch, the default), or
+    // streamed component by component inside the evaluation
+    uint32_t lw[72];
+    uint32_t pn = plist[at], cn = colj(0, pn);
+    if (g_prefetch) ml_line_load(lw, L, np, cn, el);
     auto eval = [&](r28::sp &sx, uint32_t j) {
-      const uint32_t pair = plist[at + j * stride];
-      ml_eval28(sx, L, np, colj(j, pair), P, pair, el);
+      const uint32_t pair = pn, cj = cn;
+      if (!g_prefetch) {
+        ml_eval28(sx, L, np, cj, P, Pc, pair, el);
+        if (j + 1 < cnt) pn = plist[at + (j + 1) * stride], cn = colj(j + 1, pn);
+        return;
+      }
+      ml_eval28_reg(sx, lw, np, cj, P, Pc, pair);
+      if (j + 1 < cnt) {
+        pn = plist[at + (j + 1) * stride];
+        cn = colj(j + 1, pn);
+        asm volatile("" ::: "memory");
+        ml_line_load(lw, L, np, cn, el);
+      }
     };
     eval(sa, 0);
     if (cnt == 1) {
@@ -346,17 +408,34 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
   w12_store(partial + s, acc);
 }
 
+// the pairs' G1 points by line column (Pc word w of column col[pair] at w * ncol + col): the
+// Miller kernels' point loads coalesce like their line loads
+__global__ void __launch_bounds__(WG) k_ml_pcols(const g1s *P, const uint32_t *col, uint32_t np,
+                                                 uint32_t ncol, uint32_t *Pc) {
+  const uint32_t pair = blockIdx.x * WG + threadIdx.x;
+  if (pair >= np) return;
+  const uint32_t c = col[pair];
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(P + pair);
+#pragma unroll
+  for (int i = 0; i < 36; i++) Pc[(size_t)i * ncol + c] = w[i];
+}
+void launch_ml_pcols(hipStream_t st, const g1s *P, const uint32_t *col, uint32_t np, uint32_t ncol,
+                     uint32_t *Pc) {
+  if (np) k_ml_pcols<<<nblk(np), WG, 0, st>>>(P, col, np, ncol, Pc);
+}
 void launch_ml_group(hipStream_t st, const uint32_t *lines, LineCols lc, uint32_t ngp, const g1s *P,
-                     const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
+                     const uint32_t *Pc, const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
                      int e1, fp12 *V0, uint32_t *V28) {
   dim3 grid(nblk(ngroup), e1 - e0);
   if (!ngroup || e1 <= e0) return;
   const dim3 grid1(nblk(ngroup) * (uint32_t)(e1 - e0));
   if (g_ml_r28 && V28) {
     if (g_ml_dma)
-      k_ml_group28<true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+      k_ml_group28<true, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else if (g_ml_prefetch)
+      k_ml_group28<false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     else
-      k_ml_group28<false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+      k_ml_group28<false, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     const uint32_t nvals = ngroup * (uint32_t)(e1 - e0);
     k_ml_pack28<<<nblk((size_t)nvals * 12), WG, 0, st>>>(V28, ngroup, e0, nvals, V0);
     return;

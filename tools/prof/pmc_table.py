@@ -25,7 +25,7 @@ def load(path, largest=False):
     for name, did, cn, v, gs in rows:
         if largest and gs != top[name]:
             continue
-        short = name.split("(")[0].split("::")[-1]
+        short = name.split("(")[0].split("::")[-1].replace(",", ";")
         acc.setdefault(short, {}).setdefault(cn, {})[did] = v
     return acc
 
