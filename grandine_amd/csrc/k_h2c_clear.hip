@@ -3,8 +3,9 @@
 // One DPP quad (4 lanes) per message: the doublings and additions run quad-cooperatively
 // (bls_gang.h); psi and the affine conversion run
 // redundantly in all four lanes and lane 0 stores.  Output: affine points (Miller-loop
-// input).  Launches of at least kLaneRegimeClear messages run one message per lane
-// (k_h2c_clear_lane: a quarter of the instructions per message, the chip already full).
+// input).  Launches of at least kLaneRegimeClear messages run one message per lane in two
+// kernels, one [|x|] chain each (k_h2c_clear_lane_a / _b, radix-2^28 by default: a quarter of
+// the instructions per message, the chip already full).
 #include "gbls_common.h"
 #include "bls_gang.h"
 #include "bls_w4.h"
@@ -86,18 +87,6 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_row(const g2j *Q, uint32_t n, 
   g2a o;
   jac_to_aff(o, h);
   if (l == 0) H[i] = o;
-}
-
-// one lane per message (serial clear_cofactor_g2): for launches that fill the chip
-__global__ void __launch_bounds__(WG) k_h2c_clear_lane(const g2j *Q, uint32_t n, g2a *H) {
-  uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  g2j a = Q[2 * i], b = Q[2 * i + 1], h;
-  jac_add(a, a, b);
-  clear_cofactor_g2(h, a);
-  g2a o;
-  jac_to_aff(o, h);
-  H[i] = o;
 }
 
 // The lane form in two kernels, one [|x|] chain each: in one kernel P and
