@@ -13,6 +13,7 @@
 //! A failed engine call therefore costs time, never a wrong answer or a silently kept value.
 
 use core::sync::atomic::{AtomicU64, Ordering};
+use std::sync::OnceLock;
 
 pub use bls_gpu_sys::{CallClass, EngineError, P1, P2};
 
@@ -42,6 +43,31 @@ pub(crate) fn route<T>(gpu: impl FnOnce() -> Result<T, EngineError>, cpu: impl F
     }
     CPU_FALLBACKS.fetch_add(1, Ordering::Relaxed);
     cpu()
+}
+
+/// Lone single checks -- one `verify`, one `fast_aggregate_verify`, one signature decompression,
+/// a `SingleVerifier::extend` of fewer than `SINGLE_MIN_BATCH` triples -- run on the engine only
+/// when `GBLS_SINGLE_CHECKS=engine`.  A lone check is latency-bound on the GPU (r05, idle MI355X,
+/// `profiles/r05/z_bench_c1.json`: verify 3.0 ms p50, fast_aggregate_verify over 512 keys 3.1 ms,
+/// decompression 0.58 ms; 16 threads of single verifies 3.5k/s even with cross-caller
+/// coalescing), so by default blst answers it on the calling thread; batches always go to the
+/// engine.
+pub const SINGLE_MIN_BATCH: usize = 16;
+
+#[must_use]
+pub fn single_checks_on_engine() -> bool {
+    static ON: OnceLock<bool> = OnceLock::new();
+    *ON.get_or_init(|| std::env::var("GBLS_SINGLE_CHECKS").is_ok_and(|v| v == "engine"))
+}
+
+/// `route` for a lone single check: the engine only under `GBLS_SINGLE_CHECKS=engine`, else the
+/// blst body directly (a policy choice, not a fallback: the fallback counter is not touched).
+pub(crate) fn route_single<T>(gpu: impl FnOnce() -> Result<T, EngineError>, cpu: impl FnOnce() -> T) -> T {
+    if single_checks_on_engine() {
+        route(gpu, cpu)
+    } else {
+        cpu()
+    }
 }
 
 /// Engine layout of a public key (for callers outside the crate, e.g. `MultiVerifier`).

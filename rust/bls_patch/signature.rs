@@ -8,8 +8,9 @@ impl TryFrom<SignatureBytes> for Signature {
 
     #[inline]
     fn try_from(bytes: SignatureBytes) -> Result<Self, Self::Error> {
-        // signature.rs:40-44: decompression with blst semantics (on-curve, no group check)
-        crate::gpu::route(
+        // signature.rs:40-44: decompression with blst semantics (on-curve, no group check); a lone
+        // decompression stays on blst unless GBLS_SINGLE_CHECKS=engine (crate::gpu::route_single)
+        crate::gpu::route_single(
             || {
                 bls_gpu_sys::g2_decompress(bytes.as_fixed_bytes()).map(|decoded| {
                     decoded.and_then(|point| bls_gpu_sys::signature_of_p2(&point)).map(Self)
@@ -27,7 +28,7 @@ impl Signature {
     #[must_use]
     pub fn verify(self, message: impl AsRef<[u8]>, public_key: PublicKey) -> bool {
         let message = message.as_ref();
-        crate::gpu::route(
+        crate::gpu::route_single(
             || {
                 bls_gpu_sys::verify(
                     &crate::gpu::signature_point(&self),
@@ -65,7 +66,7 @@ impl Signature {
     ) -> bool {
         let message = message.as_ref();
         let public_keys = public_keys.into_iter().collect_vec();
-        crate::gpu::route(
+        crate::gpu::route_single(
             || {
                 let points = public_keys.iter().map(|key| crate::gpu::public_key_point(key)).collect_vec();
                 bls_gpu_sys::fast_aggregate_verify(&crate::gpu::signature_point(self), message, &points)

@@ -146,6 +146,10 @@ fn extend(&mut self, triples: impl IntoIterator<Item = Triple>, signature_kind: 
     if triples.is_empty() {
         return Ok(());
     }
+    // a few triples are lone checks: blst on this thread unless GBLS_SINGLE_CHECKS=engine
+    if triples.len() < bls::gpu::SINGLE_MIN_BATCH && !bls::gpu::single_checks_on_engine() {
+        return extend_on_cpu(&triples, signature_kind);
+    }
     let (messages, signature_bytes, points, offsets) = engine_sets(&triples);
     match bls::gpu::verify_batch_compressed(&messages, &signature_bytes, &points, &offsets) {
         Some(outcomes) => {

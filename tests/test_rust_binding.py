@@ -228,7 +228,11 @@ def test_patched_bodies_fall_back_to_blst():
     route = _rust_fns(gpu.replace("pub(crate) fn route", "pub fn route"))["route"]
     assert "available()" in route and "if let Ok(value) = gpu()" in route and route.rstrip("}\n ").endswith("cpu()")
     for body, n in ((sig, 5), (pk, 2)):
-        assert body.count("crate::gpu::route(") >= n - 1
+        assert body.count("crate::gpu::route(") + body.count("crate::gpu::route_single(") >= n - 1
+    # lone single checks: blst unless GBLS_SINGLE_CHECKS=engine, then the same engine route
+    single = _rust_fns(gpu.replace("pub(crate) fn route_single", "pub fn route_single"))["route_single"]
+    assert "single_checks_on_engine()" in single and "route(gpu, cpu)" in single
+    assert sig.split("\nmod cpu {")[0].count("crate::gpu::route_single(") == 3
     for name in ("decompress", "verify", "fast_aggregate_verify", "multi_verify", "aggregate_in_place"):
         assert re.search(r"fn %s\b" % name, sig.split("\nmod cpu {")[1]), name
         assert "cpu::%s" % name in sig.split("\nmod cpu {")[0], name
