@@ -37,6 +37,9 @@ def emit_asm(terms):
     for x, y in terms:
         xi = len(ops) + 1
         ops.append(("v", x))
+        if x == y:  # a diagonal term: one operand, used twice
+            lines.append("v_mad_u64_u32 %%0, vcc, %%%d, %%%d, %%0" % (xi, xi))
+            continue
         yi = len(ops) + 1
         ops.append(("s" if y.startswith("P") else "v", y))
         lines.append("v_mad_u64_u32 %%0, vcc, %%%d, %%%d, %%0" % (xi, yi))
@@ -100,6 +103,43 @@ def emit_product(w, name, params, pairs):
     w("}")
 
 
+def emit_square(w, name):
+    """r = a^2 / 2^392: the cross terms once against the doubled limbs (d = 2a, limbs < 2^30),
+    the diagonal once: 105 product terms instead of 196 before the 196 of the reduction.
+    Column bound: 7 cross terms < 2^59 + a diagonal < 2^58 + 14 reduction terms < 2^56 < 2^63."""
+    w("__device__ __forceinline__ void %s(fe &r, const fe &a) {" % name)
+    for j in range(N):
+        w("  const uint32_t P%d = %s;" % (j, "kP28[%d]" % j))
+    w("  uint32_t d[14];")
+    w("#pragma unroll")
+    w("  for (int i = 0; i < 14; i++) d[i] = a.l[i] << 1;")
+    w("  uint32_t " + ", ".join("m%d" % j for j in range(N)) + ";")
+    w("  uint32_t t[14];")
+    w("  uint64_t acc = 0;")
+    if SPLIT:
+        w("  uint64_t acc2;")
+    for k in range(2 * N - 1):
+        ab = [("d[%d]" % i, "a.l[%d]" % (k - i)) for i in range(N) if i < k - i < N]
+        if k % 2 == 0 and k // 2 < N:
+            ab.append(("a.l[%d]" % (k // 2), "a.l[%d]" % (k // 2)))
+        mp = [("m%d" % i, "P%d" % (k - i)) for i in range(N) if i < k and 0 <= k - i < N]
+        w("  {  // column %d" % k)
+        if k < N:
+            if ab + mp:
+                w(emit_column(ab + mp))
+            w("    m%d = ((uint32_t)acc * kPinv) & kMask;" % k)
+            w(emit_asm([("m%d" % k, "P0")]))
+        else:
+            w(emit_column(ab + mp))
+            w("    t[%d] = (uint32_t)acc & kMask;" % (k - N))
+        w("    acc >>= 28;")
+        w("  }")
+    w("  t[13] = (uint32_t)acc;")
+    w("#pragma unroll")
+    w("  for (int i = 0; i < 14; i++) r.l[i] = t[i];")
+    w("}")
+
+
 def main():
     out = []
     w = out.append
@@ -111,6 +151,7 @@ def main():
     emit_product(w, "fe_mul_dev", "fe &r, const fe &a, const fe &b", (("a", "b"),))
     emit_product(w, "fe_mul2_dev", "fe &r, const fe &a, const fe &b, const fe &c, const fe &d",
                  (("a", "b"), ("c", "d")))
+    emit_square(w, "fe_sqr_dev")
     names = [("x%d" % q, "y%d" % q) for q in range(4)]
     emit_product(w, "fe_mul4_dev", "fe &r, " + ", ".join("const fe &%s, const fe &%s" % xy for xy in names),
                  tuple(names))
