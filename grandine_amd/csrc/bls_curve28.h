@@ -7,6 +7,7 @@
 // lane instead of the engine's ~1.18 (tools/ubench/r28_bench.hip).
 #pragma once
 #include "bls_curve.h"
+#include "bls_pairing.h"
 #include "bls_field28.h"
 #include "bls_r28_consts.h"
 
@@ -210,6 +211,98 @@ HD void clear_cofactor28(g2j28 &r, const g2j28 &p) {
   jac_add(t3, t3, t1);  // - psi(P)
   jac_neg(t1, p);
   jac_add(r, t3, t1);  // - P
+}
+
+// ---------------------------------------------------------------- G1 (k_mv_g1mul_lane28)
+// The same Jacobian templates over r28::fe (weakly reduced values < 1.03 p, as for fe2);
+// squarings take the dedicated radix-2^28 square (sqr: 105 + 196 product terms).
+HD void f_add(fe &r, const fe &a, const fe &b) {
+  add(r, a, b);
+  wred(r);
+}
+HD void f_sub(fe &r, const fe &a, const fe &b) { sub_r(r, a, b); }
+HD void f_mul(fe &r, const fe &a, const fe &b) { mul(r, a, b); }
+HD void f_sqr(fe &r, const fe &a) { sqr(r, a); }
+HD void f_dbl(fe &r, const fe &a) { f_add(r, a, a); }
+HD void f_zero(fe &r) {
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = 0;
+}
+HD void f_neg(fe &r, const fe &a) {
+  fe z;
+  f_zero(z);
+  sub_r(r, z, a);
+}
+HD void f_one(fe &r) { r = K28_ONE; }
+HD bool f_is_zero(const fe &a) { return is_zero(a); }
+
+typedef jac<fe> g1j28;
+
+HD void g1j28_sel(g1j28 &r, bool c, const g1j28 &a, const g1j28 &b) {  // c ? b : a
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    r.x.l[i] = c ? b.x.l[i] : a.x.l[i];
+    r.y.l[i] = c ? b.y.l[i] : a.y.l[i];
+    r.z.l[i] = c ? b.z.l[i] : a.z.l[i];
+  }
+}
+// [k] base for a 64-bit k: g1_mul_u64_w3 (bls_curve.h: signed 3-bit windows, the same
+// instructions for every lane's scalar) over r28::fe; base affine, engine form
+HD void g1_mul_u64_w3_28(g1j28 &r, const g1a &base, uint64_t k) {
+  g1j28 t0, t1, t2, t3;
+  from_fp(t0.x, base.x);
+  from_fp(t0.y, base.y);
+  f_one(t0.z);
+  if (aff_is_inf(base)) f_zero(t0.z);  // (0, 0): the point at infinity
+  jac_dbl(t1, t0);
+  jac_add(t2, t1, t0);
+  jac_dbl(t3, t1);
+  uint32_t cmask = 0, carry = 0;
+#pragma unroll
+  for (int i = 0; i < 22; i++) {
+    cmask |= carry << i;
+    carry = ((uint32_t)((k >> (3 * i)) & 7u) + carry) > 4;  // 3 i <= 63
+  }
+  g1j28 acc;
+  jac_set_inf(acc);
+  const uint32_t top = (uint32_t)(k >> 63) + (cmask >> 21);  // top digit in [0, 2]
+  g1j28_sel(acc, top == 1, acc, t0);
+  g1j28_sel(acc, top == 2, acc, t1);
+#pragma unroll 1
+  for (int i = 20; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    jac_dbl(acc, acc);
+    jac_dbl(acc, acc);
+    int v = (int)((k >> (3 * i)) & 7u) + (int)((cmask >> i) & 1u);
+    if (v > 4) v -= 8;
+    const uint32_t m = (uint32_t)(v < 0 ? -v : v);
+    g1j28 q = t0, sum;
+    g1j28_sel(q, m == 2, q, t1);
+    g1j28_sel(q, m == 3, q, t2);
+    g1j28_sel(q, m == 4, q, t3);
+    fe ny;
+    f_neg(ny, q.y);
+    if (v < 0) q.y = ny;
+    jac_add(sum, acc, q);
+    g1j28_sel(acc, m != 0, acc, sum);
+  }
+  r = acc;
+}
+// g1s_from_jac (bls_pairing.h) of a radix-2^28 point: (X Z, Y, Z^3) in engine form
+HD void g1s_from_jac28(g1s &r, const g1j28 &p) {
+  if (jac_is_inf(p)) {
+    fp_zero(r.x);
+    fp_zero(r.y);
+    fp_zero(r.c);
+    return;
+  }
+  fe z2, t;
+  sqr(z2, p.z);
+  mul(t, z2, p.z);
+  to_fp(r.c, t);
+  mul(t, p.x, p.z);
+  to_fp(r.x, t);
+  to_fp(r.y, p.y);
 }
 
 }  // namespace r28

@@ -5,6 +5,7 @@
 // S_lo = sum [lo(r_i)] sig_i, S_hi = sum [hi(r_i)] sig_i, summed by a two-level
 // workgroup tree.
 #include "gbls_common.h"
+#include "bls_curve28.h"
 #include "bls_gang.h"
 #include "bls_w4.h"
 
@@ -269,13 +270,33 @@ __global__ void __launch_bounds__(WG) k_mv_g1mul_lane(const g1a *pks, const uint
   P[i] = o;
 }
 
+// the same in radix 2^28 (bls_curve28.h g1_mul_u64_w3_28: one v_mad_u64_u32 per product term,
+// squarings by the dedicated square), the default with the other radix-2^28 lanes (g_lane_r28)
+__global__ void __launch_bounds__(WG) k_mv_g1mul_lane28(const g1a *pks, const uint64_t *rands,
+                                                        uint32_t n, g1s *P) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  const g1a pk = pks[i];
+  g1s o;
+  if (!rands) {
+    g1s_from_aff(o, pk);
+  } else {
+    r28::g1j28 t;
+    r28::g1_mul_u64_w3_28(t, pk, rands[i]);
+    r28::g1s_from_jac28(o, t);
+  }
+  P[i] = o;
+}
+
 void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint32_t n, g1s *P) {
   if (!n) return;
   if (rands && n <= kW4Max) {
     launch_mv_g1mul_w4(st, pks, rands, n, P);
     return;
   }
-  if (n >= kLaneRegimeSets)
+  if (n >= kLaneRegimeSets && g_lane_r28)
+    k_mv_g1mul_lane28<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
+  else if (n >= kLaneRegimeSets)
     k_mv_g1mul_lane<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
   else
     (nblk(4 * (size_t)n) <= w4::kExclusiveMaxWaves ? k_mv_g1mul<true> : k_mv_g1mul<false>)<<<

@@ -537,4 +537,38 @@ int h_r28_clear_check(const uint8_t *msg, uint32_t len) {
   return jac_eq(got, want) ? 1 : 0;
 }
 
+// G1 [k]P in radix 2^28 (bls_curve28.h g1_mul_u64_w3_28 + g1s_from_jac28) against the engine's
+// g1_mul_u64_w3 + g1s_from_jac: the same point up to the scaled form's Fp factor (x / c, y / c
+// compared through cross products), for n seeded (P, k); 0 = all equal
+int h_r28_g1mul_check(uint64_t seed, int n) {
+  int bad = 0;
+  for (int t = 0; t < n; t++) {
+    g1a base, gen;
+    fp_set(gen.x, k::G1X_M);
+    fp_set(gen.y, k::G1Y_M);
+    {
+      g1j g;
+      g1_mul_u64_w3(g, gen, (seed + 977 * t) | 1);
+      jac_to_aff(base, g);
+    }
+    const uint64_t k = (seed * 0x9E3779B97F4A7C15ull) ^ (0xD1B54A32D192ED03ull * (t + 1));
+    g1j want;
+    g1_mul_u64_w3(want, base, k);
+    g1s ws, gs;
+    g1s_from_jac(ws, want);
+    r28::g1j28 got;
+    r28::g1_mul_u64_w3_28(got, base, k);
+    r28::g1s_from_jac28(gs, got);
+    fp a, b;  // x_w c_g == x_g c_w, y_w c_g == y_g c_w  (c = Z^3, x = X Z)
+    fp_mul(a, ws.x, gs.c);
+    fp_mul(b, gs.x, ws.c);
+    bool ok = fp_eq(a, b);
+    fp_mul(a, ws.y, gs.c);
+    fp_mul(b, gs.y, ws.c);
+    ok = ok && fp_eq(a, b) && !fp_is_zero(gs.c);
+    bad += !ok;
+  }
+  return bad;
+}
+
 }  // extern "C"

@@ -274,3 +274,13 @@ def test_radix28_cofactor_clearing(H):
     for i in range(4):
         m = b"r28-clear/%d" % i
         assert H.h_r28_clear_check(m, len(m)) == 1, i
+
+
+def test_radix28_g1_scalar_multiplication(H):
+    """The lane-regime r_i pk_i in the radix-2^28 layer (bls_curve28.h g1_mul_u64_w3_28 over
+    r28::fe with the dedicated square, g1s_from_jac28) equals the engine's g1_mul_u64_w3 +
+    g1s_from_jac as a point (the scaled form (X Z, Y, Z^3) compared through cross products)."""
+    H.h_r28_g1mul_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    for seed in (1, 77, 0xDEADBEEF):
+        assert H.h_r28_g1mul_check(seed, 6) == 0, seed
+
