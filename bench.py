@@ -165,6 +165,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's host CPU share")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-stages", action="store_true",
+                    help="no per-stage HIP-event timing in the timed region (roofline stage times absent)")
     ap.add_argument("--no-single", action="store_true",
                     help="C2: skip the one-batch-per-step leg (PMC passes then see only the 16-batch launches)")
     ap.add_argument("--tuning", action="store_true",
@@ -423,7 +425,7 @@ def main():
         raise SystemExit("verdicts of the warm-up step are WRONG")
 
     L.gbls_profile_reset()
-    L.gbls_profile(1)
+    L.gbls_profile(0 if args.no_stages else 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -541,7 +543,7 @@ def main():
                            "parallelism": "shard sets, RCCL all-gather of Fp12 partials" if world > 1 else "1 GPU"},
                 "roofline": roof, "cpu_baseline": cpu}
         line["host_enqueue_ms"] = {"p50": round(sorted(enq)[len(enq) // 2] * 1e3, 3),
-                                   "max": round(max(enq) * 1e3, 3)}
+                                   "max": round(max(enq) * 1e3, 3), "argmax": enq.index(max(enq))}
         if cfg in ("C2", "C4", "C5"):
             line["pairings_per_s"] = round((total_units + world * leg.segments) * args.steps / dt, 1)
         if single:

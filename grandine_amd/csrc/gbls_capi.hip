@@ -100,6 +100,15 @@ const char *kStageNames[S_COUNT] = {"k_h2c_field", "k_h2c_map",   "k_h2c_clear",
                                     "k_ml_group",  "k_ml_reduce",  "k_ml_horner", "k_final_verdict",
                                     "k_pk_resolve", "k_msm"};
 
+// GBLS_TRACE_STALLS=1: report host waits inside device entry points (diagnostics)
+static bool trace_stalls() {
+  static const bool on = [] {
+    const char *e = std::getenv("GBLS_TRACE_STALLS");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
 struct Prof {
   std::mutex mu;
   std::atomic<bool> on{false};
@@ -108,8 +117,30 @@ struct Prof {
     hipEvent_t a, b;
   };
   std::vector<Rec> pending;
+  // timing events are reused (gbls_profile_read returns them here) and a batch is created when
+  // profiling is switched on, so that no hipEventCreate runs inside a profiled call: creating
+  // events while kernels run took milliseconds at times (r05 C4 enqueue stalls)
+  std::vector<hipEvent_t> free_ev;
   double ms[S_COUNT] = {0};
   uint32_t calls[S_COUNT] = {0};
+  bool take(hipEvent_t &a, hipEvent_t &b) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (free_ev.size() >= 2) {
+        a = free_ev.back();
+        free_ev.pop_back();
+        b = free_ev.back();
+        free_ev.pop_back();
+        return true;
+      }
+    }
+    if (hipEventCreate(&a) != hipSuccess) return false;
+    if (hipEventCreate(&b) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      return false;
+    }
+    return true;
+  }
 } prof;
 
 struct StageTimer {  // RAII: events around one stage's launches when profiling
@@ -118,7 +149,7 @@ struct StageTimer {  // RAII: events around one stage's launches when profiling
   int stage;
   StageTimer(int s, hipStream_t stream) : st(stream), stage(s) {
     if (!prof.on.load(std::memory_order_relaxed)) return;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+    if (!prof.take(a, b)) {
       a = b = nullptr;
       return;
     }
@@ -240,6 +271,7 @@ struct Ctx {
     stage_at = (stage_at + 1) % kStageRing;  // this call's staging buffer
     Stage &r = ring[stage_at];
     if (r.pending) {  // only when kStageRing calls of this context are still uploading
+      if (trace_stalls()) fprintf(stderr, "gbls: ctx %p waits for staging slot %d\n", (void *)this, stage_at);
       HIPCHK(hipEventSynchronize(r.ev));
       r.pending = false;
     }
@@ -264,6 +296,7 @@ struct Ctx {
   }
   bool ensure(Buf &b, size_t bytes) {
     if (bytes <= b.cap) return true;
+    if (trace_stalls()) fprintf(stderr, "gbls: ctx %p grows a buffer %zu -> %zu bytes\n", (void *)this, b.cap, bytes);
     if (!drain()) return false;
     // an in-flight stage of THIS call may still read the old buffer
     if (active) HIPCHK(hipStreamSynchronize(cur));
@@ -280,12 +313,20 @@ struct Ctx {
         r.pending = false;
       }
       if (need > r.cap) {
-        if (r.p) (void)hipHostFree(r.p);
-        r.p = nullptr;
-        r.cap = 0;
-        size_t want = std::max<size_t>(need * 2, 1 << 20);
-        if (hipHostMalloc(&r.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
-        r.cap = want;
+        const size_t want = std::max<size_t>(need * 2, 1 << 20);
+        // every idle slot of the ring grows with it: the next calls' slots are then sized by
+        // the first call of a size (a warm-up), not by the first call that reaches them --
+        // pinning pages takes milliseconds, which showed as one 18-ms enqueue among ten
+        // C4 steps (the round-5 C4 runs at ~380k instead of ~560k sets/s)
+        for (int q = 0; q < kStageRing; q++) {
+          Stage &o = ring[q];
+          if (o.cap >= want || (q != stage_at && o.pending)) continue;
+          if (o.p) (void)hipHostFree(o.p);
+          o.p = nullptr;
+          o.cap = 0;
+          if (hipHostMalloc(&o.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+          o.cap = want;
+        }
       }
       stage_used = 0;
     }
@@ -2124,6 +2165,14 @@ double gbls_measure_mad64_peak(void) {
 }
 
 int gbls_profile(int enable) {
+  if (enable) {  // a stock of timing events, created before the profiled calls
+    std::lock_guard<std::mutex> lk(prof.mu);
+    while (prof.free_ev.size() < 2048) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) break;
+      prof.free_ev.push_back(e);
+    }
+  }
   bool prev = prof.on.exchange(enable != 0);
   return prev ? 1 : 0;
 }
@@ -2136,8 +2185,8 @@ int gbls_profile_read(double *ms, uint32_t *calls, int max_stages) {
       prof.ms[r.stage] += t;
       prof.calls[r.stage] += 1;
     }
-    (void)hipEventDestroy(r.a);
-    (void)hipEventDestroy(r.b);
+    prof.free_ev.push_back(r.a);
+    prof.free_ev.push_back(r.b);
   }
   prof.pending.clear();
   int n = max_stages < S_COUNT ? max_stages : S_COUNT;
