@@ -36,8 +36,11 @@
 #include "../../include/grandine_bls_gpu.h"
 #include "gbls_common.h"
 #include "gbls_sched.h"
+#include "gbls_tables.h"
 
 using namespace gbls;
+
+static_assert(gbls::kTableWave == (uint32_t)gbls::WG, "k_ml_group wave");
 
 static_assert(sizeof(g1a) == sizeof(gbls_p1_affine), "p1 layout");
 static_assert(sizeof(g2a) == sizeof(gbls_p2_affine), "p2 layout");
@@ -55,6 +58,8 @@ namespace {
 
 constexpr int FAILED = GBLS_VERIFY_FAIL;  // engine/driver failure return (fail closed)
 constexpr size_t kShardMinSets = 1024;     // per device, before a batch is split
+// contexts per device created by gbls_init (normal, block import)
+constexpr int kPrewarmCtx[2] = {2, 1};
 
 thread_local int t_last_error = GBLS_ERR_NONE;
 
@@ -71,15 +76,21 @@ bool fail(int code) {
     }                              \
   } while (0)
 
+// the byte size a buffer grows to for `bytes`
+inline size_t grow_size(size_t bytes) { return bytes < 4096 ? 4096 : bytes + bytes / 4; }
+
 struct Buf {
   void *p = nullptr;
   size_t cap = 0;
+  bool pooled = false;  // p from hipMallocAsync (freed by hipFreeAsync)
+  // synchronous allocation (devices without stream-ordered allocation; scratch outside a lease)
   bool ensure(size_t bytes) {
     if (bytes <= cap) return true;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    pooled = false;
+    size_t want = grow_size(bytes);
     if (hipMalloc(&p, want) != hipSuccess) return false;
     cap = want;
     return true;
@@ -100,7 +111,8 @@ const char *kStageNames[S_COUNT] = {"k_h2c_field", "k_h2c_map",   "k_h2c_clear",
                                     "k_ml_group",  "k_ml_reduce",  "k_ml_horner", "k_final_verdict",
                                     "k_pk_resolve", "k_msm"};
 
-// GBLS_TRACE_STALLS=1: report host waits inside device entry points (diagnostics)
+// GBLS_TRACE_STALLS=1: report host waits inside device entry points (diagnostics); every line
+// carries the call index (leases since gbls_init) and whether the lease created its context
 static bool trace_stalls() {
   static const bool on = [] {
     const char *e = std::getenv("GBLS_TRACE_STALLS");
@@ -108,6 +120,13 @@ static bool trace_stalls() {
   }();
   return on;
 }
+std::atomic<unsigned long long> g_lease_calls{0};
+
+// Workspaces grow by stream-ordered allocation (hipMallocAsync / hipFreeAsync from the device's
+// default pool) when the device supports it: a growth never waits on the host and never frees
+// through hipFree, which synchronises the whole device (every other caller's work included).
+// Set once by engine_init.
+bool g_stream_alloc = false;
 
 struct Prof {
   std::mutex mu;
@@ -178,6 +197,14 @@ struct Ctx {
   hipEvent_t ev_fork = nullptr, ev_side1 = nullptr, ev_side2 = nullptr, ev_pks = nullptr,
              ev_done = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool done_pending = false;
+  // buffer growth: old buffers are freed and new ones allocated on `own`, ordered (GPU-side, by
+  // ev_grow) behind every other stream of the context and ahead of their later work
+  hipEvent_t ev_grow = nullptr;
+  // pinned staging buffers replaced by bigger ones: hipHostFree synchronises the device, so they
+  // are kept (growth doubles, so they total less than the live ring) instead of freed mid-call
+  std::vector<void *> retired_host;
+  unsigned long long call_id = 0;  // diagnostics: the lease's call index, and whether it
+  bool fresh = false;              // created this context
   // recorded behind this context's last kernel that read the validator registry (written under
   // the shared registry lock, read by gbls_registry_set under the exclusive one): a grown
   // registry's old table is freed only after every such reader
@@ -234,6 +261,7 @@ struct Ctx {
     HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
     for (Stage &r : ring) HIPCHK(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_reg, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_grow, hipEventDisableTiming));
     return true;
   }
   // CU-masked stream triple: mode 1 = main chain on the first `main_cus` CUs, sides on the
@@ -270,8 +298,11 @@ struct Ctx {
     active = true;
     stage_at = (stage_at + 1) % kStageRing;  // this call's staging buffer
     Stage &r = ring[stage_at];
+    if (r.pending && hipEventQuery(r.ev) == hipSuccess) r.pending = false;  // landed already
     if (r.pending) {  // only when kStageRing calls of this context are still uploading
-      if (trace_stalls()) fprintf(stderr, "gbls: ctx %p waits for staging slot %d\n", (void *)this, stage_at);
+      if (trace_stalls())
+        fprintf(stderr, "gbls: call %llu ctx %p%s waits for staging slot %d\n", call_id, (void *)this,
+                fresh ? " (fresh)" : "", stage_at);
       HIPCHK(hipEventSynchronize(r.ev));
       r.pending = false;
     }
@@ -294,13 +325,57 @@ struct Ctx {
     }
     return true;
   }
+  // every stream other than `own` this context's work may be on (the caller's stream when a call
+  // is active; it may be the legacy default stream, nullptr)
+  int other_streams(hipStream_t (&ss)[10]) {
+    int n = 0;
+    if (active && cur != own) ss[n++] = cur;
+    for (hipStream_t s : {side1, side2, own_m, side1_m, side2_m, own_g, side1_g, side2_g})
+      if (s && !(active && s == cur)) ss[n++] = s;
+    return n;
+  }
   bool ensure(Buf &b, size_t bytes) {
     if (bytes <= b.cap) return true;
-    if (trace_stalls()) fprintf(stderr, "gbls: ctx %p grows a buffer %zu -> %zu bytes\n", (void *)this, b.cap, bytes);
+    if (trace_stalls())
+      fprintf(stderr, "gbls: call %llu ctx %p%s grows a buffer %zu -> %zu bytes (%s)\n", call_id, (void *)this,
+              fresh ? " (fresh)" : "", b.cap, bytes, g_stream_alloc ? "stream-ordered" : "host wait");
+    if (g_stream_alloc) return grow_async(b, bytes) || fail(GBLS_ERR_HIP);
     if (!drain()) return false;
     // an in-flight stage of THIS call may still read the old buffer
     if (active) HIPCHK(hipStreamSynchronize(cur));
     return b.ensure(bytes) || fail(GBLS_ERR_HIP);
+  }
+  // Growth without a host wait: the old buffer is freed on `own` behind the previous call on this
+  // context (ev_done) and behind everything this call has enqueued so far on its other streams;
+  // the new one is allocated on `own`, and every other stream waits for that before its next
+  // work.  (Growth happens on a context's first calls of a size; the cross-stream waits cost
+  // overlap only then.)  No stream of its own: HIP maps streams onto a few hardware queues, and
+  // every extra stream makes two streams' packets share one more often.
+  bool grow_async(Buf &b, size_t bytes) {
+    hipStream_t ss[10];
+    const int ns = other_streams(ss);
+    if (b.p) {
+      if (done_pending) HIPCHK(hipStreamWaitEvent(own, ev_done, 0));
+      for (int i = 0; i < ns; i++) {  // one event, re-recorded: each wait takes its current record
+        HIPCHK(hipEventRecord(ev_grow, ss[i]));
+        HIPCHK(hipStreamWaitEvent(own, ev_grow, 0));
+      }
+      if (b.pooled) {
+        HIPCHK(hipFreeAsync(b.p, own));
+      } else {  // allocated before stream-ordered allocation was switched on
+        HIPCHK(hipStreamSynchronize(own));
+        HIPCHK(hipFree(b.p));
+      }
+      b.p = nullptr;
+      b.cap = 0;
+    }
+    const size_t want = grow_size(bytes);
+    HIPCHK(hipMallocAsync(&b.p, want, own));
+    b.cap = want;
+    b.pooled = true;
+    HIPCHK(hipEventRecord(ev_grow, own));
+    for (int i = 0; i < ns; i++) HIPCHK(hipStreamWaitEvent(ss[i], ev_grow, 0));
+    return true;
   }
   // bump allocation in the pinned staging buffer (per call); regrowing waits for the
   // uploads of this call that still read it
@@ -309,19 +384,27 @@ struct Ctx {
     size_t need = (bytes + 255) & ~(size_t)255;
     if (stage_used + need > r.cap) {
       if (r.pending) {
+        if (trace_stalls())
+          fprintf(stderr, "gbls: call %llu ctx %p%s waits for staging slot %d to grow it\n", call_id,
+                  (void *)this, fresh ? " (fresh)" : "", stage_at);
         if (hipEventSynchronize(r.ev) != hipSuccess) return nullptr;
         r.pending = false;
       }
       if (need > r.cap) {
         const size_t want = std::max<size_t>(need * 2, 1 << 20);
-        // every idle slot of the ring grows with it: the next calls' slots are then sized by
-        // the first call of a size (a warm-up), not by the first call that reaches them --
-        // pinning pages takes milliseconds, which showed as one 18-ms enqueue among ten
-        // C4 steps (the round-5 C4 runs at ~380k instead of ~560k sets/s)
+        // every idle slot of the ring grows with it (up to kStageShared bytes): the next calls'
+        // slots are then sized by the first call of a size (a warm-up), not by the first call
+        // that reaches them (pinning pages takes milliseconds).  Above that only this call's
+        // slot grows, so a one-off huge upload pins one buffer, not the whole ring.  Replaced
+        // buffers are retired, not freed (hipHostFree synchronises the device).
+        constexpr size_t kStageShared = 64u << 20;
         for (int q = 0; q < kStageRing; q++) {
           Stage &o = ring[q];
-          if (o.cap >= want || (q != stage_at && o.pending)) continue;
-          if (o.p) (void)hipHostFree(o.p);
+          if (o.cap >= want || (q != stage_at && (o.pending || want > kStageShared))) continue;
+          if (trace_stalls())
+            fprintf(stderr, "gbls: call %llu ctx %p%s grows staging slot %d %zu -> %zu bytes\n", call_id,
+                    (void *)this, fresh ? " (fresh)" : "", q, o.cap, want);
+          if (o.p) retired_host.push_back(o.p);
           o.p = nullptr;
           o.cap = 0;
           if (hipHostMalloc(&o.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
@@ -361,7 +444,13 @@ struct Device {
   // old buffer is freed on retire_st behind its readers (Ctx::ev_reg), never by a host wait.
   Buf reg;
   bool reg_pooled = false;  // reg.p from hipMallocAsync (freed by hipFreeAsync)
-  std::vector<void *> reg_kept;  // old tables kept when stream-ordered allocation is missing
+  // old tables when stream-ordered allocation is missing: each freed (hipFree) by a later growth
+  // once its event, recorded on retire_st behind the table's readers, has completed
+  struct Kept {
+    void *p;
+    hipEvent_t ev;
+  };
+  std::vector<Kept> reg_kept;
   hipStream_t reg_st = nullptr, retire_st = nullptr;
   hipEvent_t reg_ev = nullptr, reg_tmp = nullptr;
   bool reg_ev_set = false;
@@ -404,6 +493,11 @@ class Lease {
  public:
   Lease(Device &d, bool affine, hipStream_t stream, int cls = 0) : d_(d) {
     c_ = d.pool.acquire(affine, stream, cls, &fresh_);
+    c_->call_id = g_lease_calls.fetch_add(1);
+    c_->fresh = fresh_ || !c_->used;  // created now, or created by gbls_init and never used
+    if (fresh_ && trace_stalls())
+      fprintf(stderr, "gbls: call %llu creates ctx %p (class %d, %zu contexts)\n", c_->call_id, (void *)c_,
+              c_->cls, d.pool.size());
     ok_ = fresh_ ? c_->init(d.hipdev, g.side2_high, g.prio_mode, c_->cls)
                  : (hipSetDevice(d.hipdev) == hipSuccess || fail(GBLS_ERR_HIP));
   }
@@ -478,15 +572,54 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
   }
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
+  bool stream_alloc = true;
   for (int id : ids) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, id) != hipSuccess) return fail(GBLS_ERR_NO_DEVICE);
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return fail(GBLS_ERR_NO_DEVICE);
+    // stream-ordered allocation for the workspaces (Ctx::grow_async): the default pool keeps
+    // freed memory (no release at synchronisation points), never makes one stream's allocation
+    // wait for another stream's pending free (contexts stay independent), and is readable by
+    // the other engine devices (partials and registry slices cross devices by peer copies)
+    int pools = 0;
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, id) != hipSuccess || !pools ||
+        hipDeviceGetDefaultMemPool(&pool, id) != hipSuccess) {
+      stream_alloc = false;
+    } else {
+      uint64_t keep = UINT64_MAX;
+      int no = 0;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowInternalDependencies, &no);
+      for (int peer : ids) {
+        if (peer == id) continue;
+        hipMemAccessDesc acc{};
+        acc.location.type = hipMemLocationTypeDevice;
+        acc.location.id = peer;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        (void)hipMemPoolSetAccess(pool, &acc, 1);
+      }
+    }
     for (int r = 0; r < replicas; r++) {
       g.devs.emplace_back(new Device());
       g.devs.back()->hipdev = id;
       g.devs.back()->nsimd = 4u * (uint32_t)prop.multiProcessorCount;
       g.devs.back()->ncu = prop.multiProcessorCount;
+    }
+  }
+  (void)hipGetLastError();
+  g_stream_alloc = stream_alloc && !(flags & GBLS_INIT_TUNING && std::getenv("GBLS_SYNC_ALLOC"));
+  // contexts created up front (streams and events; workspaces grow on first use): the first
+  // concurrent callers, e.g. two submissions in flight, lease instead of creating
+  int prewarm[2] = {kPrewarmCtx[0], kPrewarmCtx[1]};
+  if (flags & GBLS_INIT_TUNING)
+    if (const char *e = std::getenv("GBLS_PREWARM")) prewarm[0] = prewarm[1] = std::atoi(e);
+  for (auto &dp : g.devs) {
+    Device &d = *dp;
+    for (int k = 0; k < prewarm[0] + prewarm[1]; k++) {
+      const int cls = k < prewarm[0] ? 0 : 1;
+      if (!d.pool.prewarm(cls, [&](Ctx &c) { return c.init(d.hipdev, g.side2_high, g.prio_mode, cls); }))
+        return fail(GBLS_ERR_HIP);
     }
   }
   // direct xGMI peer access between the engine's devices (partials gathered device-to-device,
@@ -569,125 +702,6 @@ bool resolve_pks(Ctx &c, Device &d, const PkSource &src, size_t n, hipStream_t s
   *pks = c.pks.as<g1a>();
   *pre = c.pre.as<int32_t>();
   return true;
-}
-
-// ----- Miller product tables (host side, one staged upload with the rest of a submission).
-// Level 0: per Miller segment, its pairs in groups of <= G, strided so that a wave's lanes
-// read adjacent pairs (k_ml_group); then 4-ary reduction levels down to one product per
-// segment (k_ml_reduce), whose Horner step (k_ml_horner) gives the segment's partial.
-struct MlTables {
-  struct Level {
-    size_t tab_off, nin, nout;
-  };
-  size_t plist_off = 0, grp_off = 0, ngroup = 0, v0_n = 1, v1_n = 1;
-  std::vector<Level> levels;
-  // the lines' column table (col_off: npairs entries, col[pair] = j ngp + g for pair j of group
-  // g), ngp = groups rounded up to a wave, ncol = ngp x the largest group; ngp = 0: the lines
-  // stay pair-indexed (col_off unset, ncol = npairs)
-  size_t col_off = 0;
-  uint32_t ngp = 0, ncol = 0;
-};
-// count(s): pairs of Miller segment s (>= 1); emit(s, tab): appends their pair indices.
-// npairs: pairs listed; EC: events per launch (line slices).
-template <class Count, class Emit>
-MlTables ml_tables(std::vector<uint32_t> &tab, size_t nms, size_t npairs, int EC, uint32_t nsimd,
-                   Count count, Emit emit) {
-  MlTables mt;
-  // G, the pairs per k_ml_group lane.  Small launches: the largest power of two <= 64 that
-  // still gives >= 65536 lanes per launch (EC events).  Large launches: the smallest G
-  // whose launch is at most ml_rounds waves per SIMD, EC x ceil(groups / 64) waves, so that
-  // the waves fill whole rounds of the chip's SIMDs (a launch just past a multiple of them
-  // idles most of the chip for one more wave-duration, at one wave per SIMD).
-  uint32_t G = 1;
-  while (G < 64 && (uint64_t)EC * npairs / (2 * G) >= 65536) G *= 2;
-  {
-    auto waves = [&](uint32_t gs) {
-      uint64_t ng = 0;
-      for (size_t s = 0; s < nms; s++) ng += (count(s) + gs - 1) / gs;
-      return (uint64_t)EC * ((ng + WG - 1) / WG);
-    };
-    const uint64_t cap = (uint64_t)g.ml_rounds * nsimd;
-    uint32_t lo = 1, hi = (uint32_t)std::max<size_t>(npairs, 1);  // smallest G with waves(G) <= cap
-    while (lo < hi) {
-      uint32_t mid = lo + (hi - lo) / 2;
-      if (waves(mid) <= cap)
-        hi = mid;
-      else
-        lo = mid + 1;
-    }
-    if (lo >= 8) G = lo;
-  }
-  if (g.ml_g) G = g.ml_g;
-  mt.plist_off = tab.size();
-  for (size_t s = 0; s < nms; s++) emit(s, tab);
-  mt.grp_off = tab.size();
-  std::vector<uint32_t> cnt(nms);
-  uint32_t at = 0;
-  for (size_t s = 0; s < nms; s++) {
-    const uint32_t m = count(s), ng = (m + G - 1) / G;
-    for (uint32_t k = 0; k < ng; k++) {
-      tab.push_back(at + k);
-      tab.push_back(ng);
-      tab.push_back((m - k + ng - 1) / ng);
-    }
-    cnt[s] = ng;
-    at += m;
-  }
-  mt.ngroup = (tab.size() - mt.grp_off) / 3;
-  size_t cur_n = mt.ngroup;
-  while (nms && *std::max_element(cnt.begin(), cnt.end()) > 1) {
-    MlTables::Level L{tab.size(), cur_n, 0};
-    size_t in_base = 0;
-    std::vector<uint32_t> next(nms);
-    for (size_t s = 0; s < nms; s++) {
-      const uint32_t k = cnt[s];
-      for (uint32_t q = 0; q < k; q += 4) {
-        tab.push_back((uint32_t)(in_base + q));
-        tab.push_back(std::min<uint32_t>(4, k - q));
-        next[s]++;
-      }
-      in_base += k;
-    }
-    L.nout = (tab.size() - L.tab_off) / 2;
-    mt.levels.push_back(L);
-    cnt = next;
-    cur_n = L.nout;
-  }
-  mt.v0_n = mt.ngroup;
-  for (size_t l = 0; l < mt.levels.size(); l++)
-    (l & 1 ? mt.v0_n : mt.v1_n) = std::max(l & 1 ? mt.v0_n : mt.v1_n, mt.levels[l].nout);
-  // line columns: pair j of group g at j ngp + g, so that a wave of k_ml_group (64 consecutive
-  // groups from a multiple of 64) reads 64 consecutive, 256-byte-aligned words per load
-  uint32_t gmax = 0;
-  for (size_t q = 0; q < mt.ngroup; q++) gmax = std::max(gmax, tab[mt.grp_off + 3 * q + 2]);
-  const uint32_t ngp = (uint32_t)((mt.ngroup + WG - 1) / WG * WG);
-  mt.ncol = (uint32_t)npairs;
-  if (mt.ngroup && (uint64_t)gmax * ngp < (1ull << 32)) {
-    const size_t off = tab.size();
-    tab.resize(off + npairs, 0xffffffffu);
-    bool ok = true;
-    for (size_t q = 0; q < mt.ngroup && ok; q++) {
-      const uint32_t a = tab[mt.grp_off + 3 * q], st = tab[mt.grp_off + 3 * q + 1],
-                     c = tab[mt.grp_off + 3 * q + 2];
-      for (uint32_t j = 0; j < c; j++) {
-        const uint32_t pair = tab[mt.plist_off + a + (size_t)j * st];
-        if (pair >= npairs || tab[off + pair] != 0xffffffffu) {
-          ok = false;
-          break;
-        }
-        tab[off + pair] = j * ngp + (uint32_t)q;
-      }
-    }
-    for (size_t p = 0; ok && p < npairs; p++) ok = tab[off + p] != 0xffffffffu;
-    if (ok) {  // every pair listed exactly once
-      mt.col_off = off;
-      mt.ngp = ngp;
-      mt.ncol = gmax * ngp;
-    } else {
-      tab.resize(off);
-    }
-  }
-  return mt;
 }
 
 // the reduction levels and the Horner step after k_ml_group (products in c.V0)
@@ -786,7 +800,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   MlTables mt;
   if (grouped)
     mt = ml_tables(
-        tab, nms, np, EC, d.nsimd,
+        tab, nms, np, EC, d.nsimd, g.ml_rounds, g.ml_g,
         [&](size_t s) { return 2 * (uint32_t)(std::min(n, (s + 1) * grp) - s * grp); },
         [&](size_t s, std::vector<uint32_t> &t) {
           const uint32_t b = (uint32_t)(s * grp), e = (uint32_t)std::min(n, (s + 1) * grp);
@@ -795,7 +809,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
         });
   else
     mt = ml_tables(
-        tab, nseg, np, EC, d.nsimd,
+        tab, nseg, np, EC, d.nsimd, g.ml_rounds, g.ml_g,
         [&](size_t s) { return seg_off[s + 1] - seg_off[s] + (uint32_t)X; },
         [&](size_t s, std::vector<uint32_t> &t) {
           for (uint32_t i = seg_off[s]; i < seg_off[s + 1]; i++) t.push_back(i);
@@ -1390,20 +1404,34 @@ bool registry_grow(Device &d, size_t need, size_t loaded) {
   }
   if (loaded) HIPCHK(hipMemcpyAsync(nb, d.reg.p, loaded, hipMemcpyDeviceToDevice, d.reg_st));
   HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nb) + loaded, 0, want - loaded, d.reg_st));
-  if (d.reg.p) {
-    if (d.reg_pooled) {
-      HIPCHK(hipEventRecord(d.reg_tmp, d.reg_st));
-      HIPCHK(hipStreamWaitEvent(d.retire_st, d.reg_tmp, 0));
-      bool ok = true;
-      d.pool.for_each([&](Ctx &c) {
-        if (c.reg_read && hipStreamWaitEvent(d.retire_st, c.ev_reg, 0) != hipSuccess) ok = false;
-      });
-      for (auto &o : g.devs)  // replica copies of earlier updates read device 0's table
-        if (o->reg_ev_set && hipStreamWaitEvent(d.retire_st, o->reg_ev, 0) != hipSuccess) ok = false;
-      if (!ok) return fail(GBLS_ERR_HIP);
-      HIPCHK(hipFreeAsync(d.reg.p, d.retire_st));
+  // kept tables of earlier growths (no stream-ordered allocator) whose readers have finished
+  for (size_t i = 0; i < d.reg_kept.size();) {
+    if (hipEventQuery(d.reg_kept[i].ev) == hipSuccess) {
+      (void)hipFree(d.reg_kept[i].p);
+      (void)hipEventDestroy(d.reg_kept[i].ev);
+      d.reg_kept.erase(d.reg_kept.begin() + (std::ptrdiff_t)i);
     } else {
-      d.reg_kept.push_back(d.reg.p);  // readers may still be running: kept, never host-waited
+      i++;
+    }
+  }
+  (void)hipGetLastError();
+  if (d.reg.p) {
+    HIPCHK(hipEventRecord(d.reg_tmp, d.reg_st));
+    HIPCHK(hipStreamWaitEvent(d.retire_st, d.reg_tmp, 0));
+    bool ok = true;
+    d.pool.for_each([&](Ctx &c) {
+      if (c.reg_read && hipStreamWaitEvent(d.retire_st, c.ev_reg, 0) != hipSuccess) ok = false;
+    });
+    for (auto &o : g.devs)  // replica copies of earlier updates read device 0's table
+      if (o->reg_ev_set && hipStreamWaitEvent(d.retire_st, o->reg_ev, 0) != hipSuccess) ok = false;
+    if (!ok) return fail(GBLS_ERR_HIP);
+    if (d.reg_pooled) {
+      HIPCHK(hipFreeAsync(d.reg.p, d.retire_st));
+    } else {  // readers may still be running: kept behind an event, never host-waited
+      Device::Kept k{d.reg.p, nullptr};
+      HIPCHK(hipEventCreateWithFlags(&k.ev, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(k.ev, d.retire_st));
+      d.reg_kept.push_back(k);
     }
   }
   d.reg.p = nb;
@@ -1994,15 +2022,19 @@ int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t 
       for (hipEvent_t e : v) (void)hipEventDestroy(e);
     }
   } guard{done};
+  size_t new_n = 0;  // the size this call commits
+  // a failure truncates the registry to `first`; after the lock was released (the host waits)
+  // only while no later registry_set has moved the size on from this call's
   auto broken = [&](std::unique_lock<std::shared_mutex> &wl) {
-    if (!wl.owns_lock()) wl.lock();
-    g.reg_n = std::min(g.reg_n, first);
+    const bool relock = !wl.owns_lock();
+    if (relock) wl.lock();
+    if (!relock || g.reg_n == new_n) g.reg_n = std::min(g.reg_n, first);
     fill(status, n, GBLS_BAD_ENCODING);
     return FAILED;
   };
   std::unique_lock<std::shared_mutex> wl(g.reg_mu);
   {
-    const size_t new_n = std::max(g.reg_n, first + n);
+    new_n = std::max(g.reg_n, first + n);
     if (new_n > 0xffffffffull) return fail(GBLS_ERR_ARG), FAILED;
     Device &d0 = *g.devs[0];
     for (auto &dp : g.devs) {
@@ -2012,6 +2044,15 @@ int gbls_registry_set(size_t first, const uint8_t (*pks)[48], size_t n, int32_t 
         for (auto &o : g.devs)
           if (o.get() != &d0 && o->reg_ev_set && hipStreamWaitEvent(d0.reg_st, o->reg_ev, 0) != hipSuccess)
             return fail(GBLS_ERR_HIP), broken(wl);
+      if (first < g.reg_n && new_n * sizeof(g1a) <= d.reg.cap) {
+        // loaded slots are rewritten in place: after every kernel still reading them (each
+        // context's last registry read), so no reader sees a half-written key
+        bool ok = true;
+        d.pool.for_each([&](Ctx &c) {
+          if (c.reg_read && hipStreamWaitEvent(d.reg_st, c.ev_reg, 0) != hipSuccess) ok = false;
+        });
+        if (!ok) return fail(GBLS_ERR_HIP), broken(wl);
+      }
       if (new_n * sizeof(g1a) > d.reg.cap) {
         if (!registry_grow(d, new_n * sizeof(g1a), g.reg_n * sizeof(g1a))) return broken(wl);
       } else if (first > g.reg_n &&  // a gap past the loaded keys: never-loaded slots are zero

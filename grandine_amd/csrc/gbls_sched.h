@@ -69,6 +69,21 @@ struct CtxPool {
       cv.wait(lk);  // every context of this class is leased: wait for one to come back
     }
   }
+  // a new idle context of class cls, initialised by init(ctx) before any caller can lease it
+  // (engine start: the first concurrent calls then find contexts instead of creating them)
+  template <class Init>
+  bool prewarm(int cls, Init &&init) {
+    cls = cls ? 1 : 0;
+    std::unique_ptr<Ctx> c(new Ctx());
+    c->cls = cls;
+    if (!init(*c)) return false;
+    std::lock_guard<std::mutex> lk(mu);
+    if (count[cls] >= kMaxCtx[cls]) return false;
+    count[cls]++;
+    idle.push_back(c.get());
+    all.push_back(std::move(c));
+    return true;
+  }
   void release(Ctx *c) {
     {
       std::lock_guard<std::mutex> lk(mu);

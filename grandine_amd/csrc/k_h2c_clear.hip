@@ -161,6 +161,15 @@ __device__ __forceinline__ void g2j28_load(r28::g2j28 &r, const g2j &src) {
   r28::load12(r.y.c0, src.y.c0), r28::load12(r.y.c1, src.y.c1);
   r28::load12(r.z.c0, src.z.c0), r28::load12(r.z.c1, src.z.c1);
 }
+// A chain's base point in LDS, one per lane at an ODD stride of 85 words (84 + 1 pad): the 4-byte
+// LDS accesses of the 32 lanes of a group then fall in 32 different banks (the unpadded stride
+// of 84 = 4 x 21 words put every 4th lane on one bank: 4-way conflicts, 58 % of the kernels'
+// LDS cycles in the r05 PMC pass, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE)
+struct g2j28_lds {
+  r28::g2j28 v;
+  uint32_t pad;
+};
+static_assert(sizeof(g2j28_lds) == 85 * 4, "odd LDS stride");
 // h = [|x|] (*pl), the base read from LDS at each of the 5 additions
 __device__ __forceinline__ void mul_by_xabs28(r28::g2j28 &h, const r28::g2j28 *pl) {
   h = *pl;
@@ -172,8 +181,8 @@ __device__ __forceinline__ void mul_by_xabs28(r28::g2j28 &h, const r28::g2j28 *p
 __global__ void __launch_bounds__(WG) k_h2c_clear_lane_a28(g2j *Q, uint32_t n) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
-  __shared__ r28::g2j28 pl[WG];
-  r28::g2j28 *pp = pl + threadIdx.x;
+  __shared__ g2j28_lds pl[WG];
+  r28::g2j28 *pp = &pl[threadIdx.x].v;
   r28::g2j28 t1;
   {
     r28::g2j28 p, q;
@@ -209,8 +218,8 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane_a28(g2j *Q, uint32_t n) {
 __global__ void __launch_bounds__(WG) k_h2c_clear_lane_b28(const g2j *Q, uint32_t n, g2a *H) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
-  __shared__ r28::g2j28 pl[WG];
-  r28::g2j28 *pp = pl + threadIdx.x;
+  __shared__ g2j28_lds pl[WG];
+  r28::g2j28 *pp = &pl[threadIdx.x].v;
   r28::g2j28 h;
   {
     r28::g2j28 t2;

@@ -246,8 +246,15 @@ __global__ void __launch_bounds__(WG) k_lines_lane28(const g2a *H, uint32_t firs
     lines_range(L, np, cp, Q, e0, e1, Ts);  // identity lines (engine form)
     return;
   }
-  __shared__ r28::fe2 qs[2 * WG];
-  r28::fe2 &qx = qs[threadIdx.x], &qy = qs[WG + threadIdx.x];
+  // Q's coordinates in LDS at an odd stride of 29 words per lane (28 + 1 pad): conflict-free
+  // 4-byte accesses (the unpadded 28-word stride put every 8th lane of a group on one bank)
+  struct fe2_lds {
+    r28::fe2 v;
+    uint32_t pad;
+  };
+  static_assert(sizeof(fe2_lds) == 29 * 4, "odd LDS stride");
+  __shared__ fe2_lds qs[2 * WG];
+  r28::fe2 &qx = qs[threadIdx.x].v, &qy = qs[WG + threadIdx.x].v;
   r28::g2h28 T;
   r28::from_fp(T.x.c0, Q.x.c0);
   r28::from_fp(T.x.c1, Q.x.c1);

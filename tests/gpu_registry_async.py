@@ -5,9 +5,12 @@ verifications are still running on a device stream (VERDICT r04 "next 5").
 * two indexed multi_verify submissions of 131072 sets each (~30 ms of GPU work apiece) are
   queued on two torch streams (gbls_multi_verify_indexed_segments_device: asynchronous, reading
   the registry), the second with one swapped signature;
-* registry_set then loads keys far past the table's capacity (the table is reallocated and the
-  old one retired behind those readers on the GPU) and must return while the stream is still
-  busy -- no device-wide synchronisation, no host wait for other callers' work;
+* the two streams are HELD by a host-released gate (tests/hip_gate.py: hipStreamWaitValue32 on
+  a pinned word) before the submissions are queued, so none of their work can run until the
+  host opens it; registry_set then loads keys far past the table's capacity (the table is
+  reallocated and the old one retired behind those readers on the GPU) and must RETURN while the
+  gate is still closed -- any device-wide synchronisation or host wait for those readers would
+  block it (a watchdog opens the gate after 60 s and the test fails): ordering, not wall-clock;
 * every queued verdict must be right (the readers kept a valid table), and afterwards sets over
   the old slots and over the new slice verify (the loaded entries were carried over).
 Also replicas (gbls_init flags & 0xff = 2): the same growth on two engines of the one GPU.
@@ -16,6 +19,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -24,6 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from grandine_amd import _lib as G  # noqa: E402
 from grandine_amd import factory as F  # noqa: E402
+from hip_gate import Gate  # noqa: E402  (tests/, the script's own directory)
 
 
 def main():
@@ -57,27 +62,39 @@ def main():
     new_sks, new_comp = F.registry(64, seed=b"async-new")
     verdicts.fill_(-1)
     torch.cuda.synchronize()
-    t_q = time.perf_counter()
-    for j in range(k):
-        s = streams[j % nst]
-        with torch.cuda.stream(s):
-            G.check(L.gbls_multi_verify_indexed_segments_device(
-                d_msgs.data_ptr(), (d_bad if j % 3 == 1 else d_sigs).data_ptr(), d_idx.data_ptr(), None,
-                d_r.data_ptr(), n, off, 1, verdicts[j:].data_ptr(), ctypes.c_void_p(s.cuda_stream)), "queued")
-    enq_ms = 1e3 * (time.perf_counter() - t_q)
-    busy_before_set = any(not s.query() for s in streams)
-    # growth while they run: 64 new keys at index 400000 (the table holds ~5k), made beforehand
     first = 400_000
     st = (ctypes.c_int32 * 64)()
-    t0 = time.perf_counter()
-    rc = L.gbls_registry_set(first, G.buf(new_comp), 64, st)
-    t_set = time.perf_counter() - t0
-    busy_after_set = any(not s.query() for s in streams)
+    out = {}
+
+    def queue_and_set():
+        t_q = time.perf_counter()
+        for j in range(k):
+            s = streams[j % nst]
+            with torch.cuda.stream(s):
+                G.check(L.gbls_multi_verify_indexed_segments_device(
+                    d_msgs.data_ptr(), (d_bad if j % 3 == 1 else d_sigs).data_ptr(), d_idx.data_ptr(), None,
+                    d_r.data_ptr(), n, off, 1, verdicts[j:].data_ptr(), ctypes.c_void_p(s.cuda_stream)), "queued")
+        out["enqueue_ms"] = round(1e3 * (time.perf_counter() - t_q), 3)
+        # growth while the readers are held: 64 new keys at index 400000 (the table holds ~5k)
+        t0 = time.perf_counter()
+        out["rc"] = L.gbls_registry_set(first, G.buf(new_comp), 64, st)
+        out["set_ms"] = round(1e3 * (time.perf_counter() - t0), 3)
+
+    gate = Gate()
+    try:
+        for s in streams:
+            gate.hold(s.cuda_stream)
+        worker = threading.Thread(target=queue_and_set, daemon=True)
+        worker.start()
+        worker.join(timeout=60)
+        returned_while_held = not worker.is_alive()
+        held_busy = all(not s.query() for s in streams)  # the gate still holds every reader
+    finally:
+        gate.release()
+    worker.join(timeout=120)
     torch.cuda.synchronize()
-    t_all = time.perf_counter() - t0
-    res = {"rc": rc, "statuses": sorted(set(st)), "busy_after_set": busy_after_set,
-           "busy_before_set": busy_before_set, "enqueue_ms": round(enq_ms, 3),
-           "set_ms": round(1e3 * t_set, 3), "queue_ms": round(1e3 * t_all, 3),
+    res = {"rc": out.get("rc"), "statuses": sorted(set(st)), "returned_while_held": returned_while_held,
+           "held_busy": held_busy, "enqueue_ms": out.get("enqueue_ms"), "set_ms": out.get("set_ms"),
            "verdicts": verdicts.cpu().tolist(), "size": L.gbls_registry_size(), "cap0": cap0,
            "replicas": L.gbls_device_count()}
     # old slots and the new slice both resolve after the growth

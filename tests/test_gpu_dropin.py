@@ -253,19 +253,48 @@ def test_policy_flags_are_sticky(G, L, F):
         L.gbls_set_policy(prev)
 
 
+def gate_env(**extra):
+    """Environment of a subprocess that holds streams with tests/hip_gate.py.  A held stream
+    blocks the hardware queue it is mapped to, and HIP maps streams onto GPU_MAX_HW_QUEUES queues
+    (4 by default): with 32, every stream of these small processes gets a queue of its own, so
+    only the held streams (and work that waits on them) are blocked."""
+    return dict(os.environ, GPU_MAX_HW_QUEUES="32", **extra)
+
+
 @pytest.mark.parametrize("replicas", [1, 2])
 def test_registry_growth_during_inflight_verifies_subprocess(replicas):
     """VERDICT r04 "next 5": gbls_registry_set with growth returns while indexed verifications
     are still running on another stream; their verdicts are right and the table keeps its
     entries (tests/gpu_registry_async.py, its own engine)."""
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_registry_async.py"), str(replicas)],
-                         capture_output=True, text=True, timeout=300)
+                         capture_output=True, text=True, timeout=300, env=gate_env())
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])
     print(res)
     assert res["rc"] == 0 and res["statuses"] == [0] and res["replicas"] == replicas
     assert res["verdicts"] == [0, 5]
-    # no device-wide stall and no wait for other callers' work inside registry_set: it returns
-    # while the queued verifications still run (its own small kernels only need free SIMDs)
-    assert res["busy_before_set"] and res["busy_after_set"], res
+    # no device-wide stall and no wait for other callers' work inside the enqueues or
+    # registry_set: both returned while a host gate still held every reader stream (ordering,
+    # independent of workload size and timing)
+    assert res["returned_while_held"] and res["held_busy"], res
     assert res["size"] == 400_064 and res["after"] == 0 and res["gap"] == 5
+
+
+def test_fresh_context_growth_does_not_wait_for_other_streams_subprocess():
+    """VERDICT r05 "next 1": a context's first call grows every workspace without waiting for
+    other streams: while a host gate holds stream A (a verification queued behind it), a call on
+    stream B that leases a never-used context returns AND completes with the right verdict; A is
+    provably still held meanwhile, and verifies once released (tests/gpu_fresh_ctx.py)."""
+    env = gate_env(GBLS_TRACE_STALLS="1")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_fresh_ctx.py")],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    print(res)
+    print(out.stderr[-3000:])
+    assert res["rc_a"] == 0 and res["rc_b"] == 0, res
+    assert res["finished_while_held"] and res["a_busy_while_held"], res
+    assert res["v_b_while_held"] == 0 and res["verdicts"] == [0, 0], res
+    # the growth was stream-ordered and B's context was a first-use one
+    assert "(fresh) grows a buffer" in out.stderr and "(stream-ordered)" in out.stderr, out.stderr[-2000:]
+    assert "(host wait)" not in out.stderr, out.stderr[-2000:]

@@ -53,3 +53,20 @@ def test_scheduling_under_tsan(tmp_path):
     assert out.returncode == 0, log
     assert "ThreadSanitizer" not in out.stderr, log
     assert "sched_tsan: OK" in out.stdout, log
+
+
+def test_miller_tables_under_asan(tmp_path):
+    """the Miller product tables (grandine_amd/csrc/gbls_tables.h, built by
+    every pipeline) keep the line buffer within 1.25x the event-slice budget also for uneven
+    segment mixes (one large segment beside thousands of one- and two-set segments), never put a
+    whole large segment in one lane, list every pair once and give each its column
+    (tests/native/tables_check.cpp, under ASan/UBSan)."""
+    exe = str(tmp_path / "tables_check")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=all", "-Wall", "-Wextra", "-Werror",
+                           "-I", os.path.join(ROOT, "grandine_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "native", "tables_check.cpp"), "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    log = out.stdout[-3000:] + out.stderr[-3000:]
+    assert out.returncode == 0, log
+    assert "tables_check: OK" in out.stdout, log
