@@ -164,6 +164,9 @@ def main():
                          "the engine's coalescer merges concurrent callers")
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's host CPU share")
+    ap.add_argument("--emulate-shard", type=int, default=0,
+                    help="C4 on one GPU: verify only rank 0's committees of an N-way split (its per-GPU "
+                         "shard shape) and report the node rate that shape predicts (DESIGN.md 5)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stages", action="store_true",
                     help="no per-stage HIP-event timing in the timed region (roofline stage times absent)")
@@ -253,7 +256,12 @@ def main():
             sks, comp = F.registry(nreg, seed=b"c4-registry")
             assert not F.load_registry(comp).any()
             idx_all, off_all = F.committees(nact, ncom_all, seed=4)
-            c0, c1 = ncom_all * rank // world, ncom_all * (rank + 1) // world
+            shard = world
+            if args.emulate_shard:
+                if world != 1:
+                    raise SystemExit("--emulate-shard runs on one GPU")
+                shard = args.emulate_shard
+            c0, c1 = ncom_all * rank // shard, ncom_all * (rank + 1) // shard
             idx = idx_all[off_all[c0]:off_all[c1]]
             off = (off_all[c0:c1 + 1] - off_all[c0]).astype(np.uint32)
             msgs = F.messages(ncom_all, b"c4")[32 * c0:32 * c1]
@@ -463,8 +471,9 @@ def main():
         good = torch.tensor([int((vc == G.SUCCESS).sum().item())], dtype=torch.int64, device=dev)
         if world > 1:
             dist.all_reduce(good, op=dist.ReduceOp.SUM)
-        committee_check = {"committees_verified": int(good.item()), "committees": leg.epoch["committees"]}
-        if committee_check["committees_verified"] != leg.epoch["committees"]:
+        expect = n if args.emulate_shard else leg.epoch["committees"]
+        committee_check = {"committees_verified": int(good.item()), "committees": expect}
+        if committee_check["committees_verified"] != expect:
             raise SystemExit("per-committee verdicts WRONG: %s" % committee_check)
 
     # ---- one batch per step (the 4096-set latency view), same inputs, after the main timing
@@ -550,7 +559,19 @@ def main():
             line["single_batch"] = single
         if getattr(leg, "grouped", None):
             line["config"]["grouped_checks"] = leg.grouped
-        if cfg == "C4":
+        if cfg == "C4" and args.emulate_shard:
+            # one rank's shard of an N-way split on this GPU: its own rate, and the node rate the
+            # shape predicts when every rank runs its shard in the same time (the all-gather of
+            # 576-B partials and the one final exponentiation are not included)
+            per_rank = leg.units
+            line["value"] = round(per_rank * args.steps / dt, 1)
+            line["config"]["workload"] = ("C4 shard emulation: rank 0's %d of %d committees (a %d-way split) on one "
+                                          "GPU" % (per_rank, leg.epoch["committees"], args.emulate_shard))
+            line["shard_emulation"] = {"n_gpus_emulated": args.emulate_shard, "committees_per_rank": per_rank,
+                                       "ms_per_step": round(dt / args.steps * 1e3, 4),
+                                       "predicted_node_sets_per_s": round(leg.epoch["committees"] * args.steps / dt, 1)}
+            line["epoch"] = dict(leg.epoch, per_committee_check=committee_check)
+        elif cfg == "C4":
             line["pks_aggregated_per_s"] = round(leg.epoch["keys"] * args.steps / dt, 1)
             line["epoch"] = dict(leg.epoch, per_committee_check=committee_check)
         print(json.dumps(line), flush=True)

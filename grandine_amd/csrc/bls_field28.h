@@ -578,6 +578,57 @@ HD void fe12_mul_034_lazy_st(fe12 &f, const sp &s, uint32_t *st, uint32_t stride
   fe2_unstash(f5, st + 56 * stride, stride);
 }
 
+// ---- r06: the same product with Karatsuba Fp2 products (fe2_mul3k: 9 products of 196 terms per
+// output Fp2 coordinate instead of 12; tools/gen_fpmul28.py emit_kara3).  Each output r_k (Fp2)
+// is x_1 u_1 + x_2 u_2 + x_3 u_3 with x from f and u a line coefficient; the line's limbwise
+// sums us = u.c0 + u.c1 are formed once per line, f's inside the product.  Outputs < 1.03 p
+// (the c0 coordinate carries a bias of 17 p^2, a multiple of p), normalized.
+HD void fe2_sum(fe &r, const fe2 &a) { add_lazy(r, a.c0, a.c1); }  // limbs < 2^29
+HD void fe2_mul3k(fe2 &r, const fe2 &x0, const fe2 &u0, const fe &u0s, const fe2 &x1, const fe2 &u1,
+                  const fe &u1s, const fe2 &x2, const fe2 &u2, const fe &u2s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe2_mul3k_dev(r.c0, r.c1, x0.c0, x0.c1, u0.c0, u0.c1, u0s, x1.c0, x1.c1, u1.c0, u1.c1, u1s, x2.c0, x2.c1, u2.c0,
+                u2.c1, u2s);
+#else
+  (void)u0s, (void)u1s, (void)u2s;  // the host computes the same value (mod p) the schoolbook way
+  fe n0, n1, n2;
+  neg_lazy(n0, u0.c1);
+  neg_lazy(n1, u1.c1);
+  neg_lazy(n2, u2.c1);
+  fe2_mul3_acc(r, x0, u0, n0, x1, u1, n1, x2, u2, n2);
+#endif
+}
+HD void fe12_mul_034_kara_st(fe12 &f, const sp &s, uint32_t *st, uint32_t stride) {
+  fe2 &f0 = f.c0.c0, &f1 = f.c1.c0, &f2 = f.c0.c1, &f3 = f.c1.c1, &f4 = f.c0.c2, &f5 = f.c1.c2;
+  fe s0, s2, s3;
+  fe2_sum(s0, s.a0);
+  fe2_sum(s2, s.a2);
+  fe2_sum(s3, s.a3);
+  fe2 x;
+  fe2_mul3k(x, f3, s.a0, s0, f1, s.a2, s2, f0, s.a3, s3);
+  fe2_stash(st, stride, x);  // r3
+  fe2_mul3k(x, f4, s.a0, s0, f2, s.a2, s2, f1, s.a3, s3);
+  fe2_stash(st + 28 * stride, stride, x);  // r4
+  fe2_mul3k(x, f5, s.a0, s0, f3, s.a2, s2, f2, s.a3, s3);
+  fe2_stash(st + 56 * stride, stride, x);  // r5
+  fe2 b3, b2;
+  sub(b3.c0, s.a3.c0, s.a3.c1);  // xi a3 (< 5.1 p, normalized)
+  add(b3.c1, s.a3.c0, s.a3.c1);
+  fe2_sum(s3, b3);
+  fe2_mul3k(x, f2, s.a0, s0, f0, s.a2, s2, f5, b3, s3);
+  f2 = x;  // r2
+  sub(b2.c0, s.a2.c0, s.a2.c1);  // xi a2
+  add(b2.c1, s.a2.c0, s.a2.c1);
+  fe2_sum(s2, b2);
+  fe2_mul3k(x, f0, s.a0, s0, f4, b2, s2, f3, b3, s3);
+  f0 = x;  // r0
+  fe2_unstash(f3, st, stride);
+  fe2_mul3k(x, f1, s.a0, s0, f5, b2, s2, f4, b3, s3);
+  f1 = x;  // r1
+  fe2_unstash(f4, st + 28 * stride, stride);
+  fe2_unstash(f5, st + 56 * stride, stride);
+}
+
 // (a0 + a2 w^2 + a3 w^3)(b0 + b2 w^2 + b3 w^3) with one reduction per output Fp coordinate:
 //   r0 = a0 b0 + a3 (xi b3), r1 = 0, r2 = a0 b2 + a2 b0, r3 = a0 b3 + a3 b0, r4 = a2 b2,
 //   r5 = a2 b3 + a3 b2

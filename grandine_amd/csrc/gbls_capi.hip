@@ -52,14 +52,25 @@ uint32_t gbls::g_msm_k = gbls::kMsmChunk;
 uint32_t gbls::g_ml_xcd = 1;
 uint32_t gbls::g_ml_dma = 0;
 uint32_t gbls::g_ml_prefetch = 1;
+uint32_t gbls::g_ml_kara = 0;
 uint32_t gbls::g_lane_r28 = 1;
 
 namespace {
 
 constexpr int FAILED = GBLS_VERIFY_FAIL;  // engine/driver failure return (fail closed)
 constexpr size_t kShardMinSets = 1024;     // per device, before a batch is split
-// contexts per device created by gbls_init (normal, block import)
-constexpr int kPrewarmCtx[2] = {2, 1};
+// contexts per device created by gbls_init (normal, block import).  Measured r06
+// (profiles/r06/README.md, tools/gpu/ab_c2c4.sh): HIP binds every stream to a hardware queue of
+// its priority when the stream is created (up to GPU_MAX_HW_QUEUES per priority), and the set of
+// queues a process holds moves the default bench by several per cent.  Two normal contexts (two
+// submissions in flight) plus the registry's high-priority update stream, created here in that
+// order, measured best on every leg in one box: C2 4.37-4.40M sets/s, a single 4096-set batch
+// 779-790k, C4 525-537k.  With the block context as well (3 more high-priority queues) the single
+// batch drops to ~690k; with one more normal-priority queue (the registry's retire stream, now
+// created by the first table growth) to ~685k; without the third high-priority queue C2 varies
+// 4.20-4.35M; and creating contexts inside a timed loop costs C4 a third (350-390k).
+// Block-import contexts are created by the first block import.
+constexpr int kPrewarmCtx[2] = {2, 0};
 
 thread_local int t_last_error = GBLS_ERR_NONE;
 
@@ -522,6 +533,8 @@ class Lease {
   bool fresh_ = false, ok_ = false;
 };
 
+bool registry_streams(Device &d);
+
 bool engine_init(uint32_t device_mask, uint32_t flags) {
   std::lock_guard<std::mutex> lk(g.mu);
   // policy flags are sticky: a gbls_init that names one turns it on, also on an engine that is
@@ -569,6 +582,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_ML_R28")) g_ml_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_ML_DMA")) g_ml_dma = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_ML_PREFETCH")) g_ml_prefetch = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_ML_KARA")) g_ml_kara = (uint32_t)std::strtoul(e, nullptr, 10);
   }
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
@@ -613,13 +627,43 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
   // concurrent callers, e.g. two submissions in flight, lease instead of creating
   int prewarm[2] = {kPrewarmCtx[0], kPrewarmCtx[1]};
   if (flags & GBLS_INIT_TUNING)
-    if (const char *e = std::getenv("GBLS_PREWARM")) prewarm[0] = prewarm[1] = std::atoi(e);
+    if (const char *e = std::getenv("GBLS_PREWARM")) {  // "normal[,block]"
+      prewarm[0] = prewarm[1] = std::atoi(e);
+      if (const char *c = std::strchr(e, ',')) prewarm[1] = std::atoi(c + 1);
+    }
+  // experiments (tuning only): GBLS_PREWARM_BLOCK_FIRST=1 creates the block-class contexts
+  // first; GBLS_DUMMY_STREAMS=n,prio creates n idle streams of priority prio (0 high, 1 low,
+  // 2 default) after the contexts (HIP maps streams onto hardware queues per priority)
+  const bool block_first = (flags & GBLS_INIT_TUNING) && std::getenv("GBLS_PREWARM_BLOCK_FIRST");
   for (auto &dp : g.devs) {
     Device &d = *dp;
     for (int k = 0; k < prewarm[0] + prewarm[1]; k++) {
-      const int cls = k < prewarm[0] ? 0 : 1;
+      const int cls = block_first ? (k < prewarm[1] ? 1 : 0) : (k < prewarm[0] ? 0 : 1);
       if (!d.pool.prewarm(cls, [&](Ctx &c) { return c.init(d.hipdev, g.side2_high, g.prio_mode, cls); }))
         return fail(GBLS_ERR_HIP);
+    }
+    // the registry's streams at start as well (one high-priority stream for its updates, one for
+    // retiring old tables), not at the first gbls_registry_set; the update stream is touched
+    // here so that it holds its hardware queue from the start (HIP binds a stream's queue at
+    // its first use), which is the queue set measured best above
+    const bool reg_at_init = !((flags & GBLS_INIT_TUNING) && std::getenv("GBLS_REG_AT_INIT") &&
+                               std::atoi(std::getenv("GBLS_REG_AT_INIT")) == 0);
+    if (reg_at_init && (!registry_streams(d) || hipStreamQuery(d.reg_st) != hipSuccess))
+      return fail(GBLS_ERR_HIP);
+    if (const char *e = (flags & GBLS_INIT_TUNING) ? std::getenv("GBLS_DUMMY_STREAMS") : nullptr) {
+      int least = 0, greatest = 0;
+      (void)hipSetDevice(d.hipdev);
+      (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+      const char *c = std::strchr(e, ',');
+      const int pr = c ? std::atoi(c + 1) : 0;
+      for (int k = std::atoi(e); k > 0; k--) {
+        hipStream_t s = nullptr;
+        if (pr == 2)
+          (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        else
+          (void)hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pr == 0 ? greatest : least);
+        if (s) (void)hipStreamQuery(s);
+      }
     }
   }
   // direct xGMI peer access between the engine's devices (partials gathered device-to-device,
@@ -1384,7 +1428,6 @@ bool registry_streams(Device &d) {
   int least = 0, greatest = 0;  // registry updates are small: they jump the queued normal work
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   HIPCHK(hipStreamCreateWithPriority(&d.reg_st, hipStreamNonBlocking, greatest));
-  HIPCHK(hipStreamCreateWithFlags(&d.retire_st, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&d.reg_ev, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&d.reg_tmp, hipEventDisableTiming));
   return true;
@@ -1416,6 +1459,9 @@ bool registry_grow(Device &d, size_t need, size_t loaded) {
   }
   (void)hipGetLastError();
   if (d.reg.p) {
+    // the retire stream is created by the first growth that retires a table (a stream holds a
+    // hardware queue from its creation; the engine's queue set is tuned, see kPrewarmCtx)
+    if (!d.retire_st) HIPCHK(hipStreamCreateWithFlags(&d.retire_st, hipStreamNonBlocking));
     HIPCHK(hipEventRecord(d.reg_tmp, d.reg_st));
     HIPCHK(hipStreamWaitEvent(d.retire_st, d.reg_tmp, 0));
     bool ok = true;

@@ -43,6 +43,7 @@ constexpr uint32_t kMsmChunk = 16;
 constexpr int kMsmFoldLevels = 3;        // k_msm_fold: pairwise levels over each bucket's partials
 constexpr uint32_t kMsmFold = 1u << kMsmFoldLevels;  // chunk partials per fold group
 extern uint32_t g_msm_k;                 // kMsmChunk unless GBLS_MSM_K is set
+extern uint32_t g_ml_kara;               // k_ml_group28: Karatsuba Fp2 sparse products (GBLS_ML_KARA)
 extern uint32_t g_ml_prefetch;           // k_ml_group28: next pair's line loaded during the product (GBLS_ML_PREFETCH)
 extern uint32_t g_ml_dma;                // k_ml_group28: line staged in LDS by DMA loads (GBLS_ML_DMA)
 extern uint32_t g_ml_xcd;                // k_ml_group: XCD-grouped block order (GBLS_ML_XCD)

@@ -106,8 +106,46 @@ __device__ __forceinline__ void ml_pword(fp &r, const g1s *P, const uint32_t *Pc
     for (int i = 0; i < 12; i++) r.l[i] = w[i];
   }
 }
+// The points by line column (Pc, k_ml_pcols) are NORMALIZED since r06: (x, y, c) = (2^8 xP,
+// 2^8 yP, 1) for P = (xP, yP), all zero for infinity.  A line (L0 c + L2 x w^2 + L3 y w^3) then
+// needs 4 products instead of 6: a0 is L0 itself, read as radix-2^28 limbs (L0 2^-8 in that
+// reading), and L2 x, L3 y over 2^392 carry the same 2^-8 (the point's 2^8 cancels one of the two
+// 2^-8 of the reading): one Fp* scalar per line, which the final exponentiation removes.  The
+// infinity test reads one word of c (the Montgomery one's low word is nonzero).
+__device__ __forceinline__ bool ml_pc_inf(const uint32_t *Pc, uint32_t np, uint32_t col) {
+  return Pc[(size_t)24 * np + col] == 0;
+}
+template <bool PCN>
 __device__ __forceinline__ void ml_eval28(r28::sp &s, const uint32_t *L, uint32_t np, uint32_t col,
                                           const g1s *P, const uint32_t *Pc, uint32_t pair, int e) {
+  if constexpr (PCN) {  // normalized point: a0 = L0 read directly, 4 products
+    if (ml_pc_inf(Pc, np, col)) {
+      r28::sp_identity(s);
+      return;
+    }
+    r28::fe *out[6] = {&s.a0.c0, &s.a0.c1, &s.a2.c0, &s.a2.c1, &s.a3.c0, &s.a3.c1};
+    fp w, pxy;
+    ml_pword(pxy, P, Pc, np, col, pair, 0);  // x, for L2
+    r28::fe q;
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+#pragma unroll
+      for (int i = 0; i < 12; i++) w.l[i] = L[line_word(e, c, i, np, col)];
+      if (c == 2) r28::repack_in(q, pxy);
+      if (c == 2) ml_pword(pxy, P, Pc, np, col, pair, 1);  // y, for L3
+      if (c == 4) r28::repack_in(q, pxy);
+      asm volatile("" ::: "memory");
+      if (c < 2) {
+        r28::repack_in(*out[c], w);
+      } else {
+        r28::fe t;
+        r28::repack_in(t, w);
+        r28::mul(*out[c], t, q);
+      }
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
   fp pc;
   ml_pword(pc, P, Pc, np, col, pair, 2);
   if (fp_is_zero(pc)) {
@@ -150,9 +188,39 @@ __device__ __forceinline__ void ml_line_load(uint32_t (&lw)[72], const uint32_t 
   for (int w = 0; w < 72; w++) lw[w] = L[line_word(e, w / 12, w % 12, np, col)];
 }
 // ml_eval28 on a loaded line
+template <bool PCN>
 __device__ __forceinline__ void ml_eval28_reg(r28::sp &s, const uint32_t (&lw)[72], uint32_t np,
                                               uint32_t col, const g1s *P, const uint32_t *Pc,
                                               uint32_t pair) {
+  if constexpr (PCN) {  // normalized point (see ml_eval28): a0 = L0 read directly, 4 products
+    if (ml_pc_inf(Pc, np, col)) {
+      r28::sp_identity(s);
+      return;
+    }
+    r28::fe *out[6] = {&s.a0.c0, &s.a0.c1, &s.a2.c0, &s.a2.c1, &s.a3.c0, &s.a3.c1};
+    fp pxy;
+    ml_pword(pxy, P, Pc, np, col, pair, 0);  // x, for L2
+    r28::fe q;
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      if (c == 2) r28::repack_in(q, pxy);
+      if (c == 2) ml_pword(pxy, P, Pc, np, col, pair, 1);  // y, for L3
+      if (c == 4) r28::repack_in(q, pxy);
+      asm volatile("" ::: "memory");
+      fp w;
+#pragma unroll
+      for (int i = 0; i < 12; i++) w.l[i] = lw[12 * c + i];
+      if (c < 2) {
+        r28::repack_in(*out[c], w);
+      } else {
+        r28::fe t;
+        r28::repack_in(t, w);
+        r28::mul(*out[c], t, q);
+      }
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
   fp pc;
   ml_pword(pc, P, Pc, np, col, pair, 2);
   if (fp_is_zero(pc)) {
@@ -230,7 +298,7 @@ __device__ __forceinline__ void dma_wait() {
 }
 __device__ __forceinline__ void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <bool DMA, bool g_prefetch>
+template <bool DMA, bool g_prefetch, bool KARA = false, bool PCN = false>
 __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, LineCols lc, uint32_t ngp, const g1s *P,
                                                    const uint32_t *Pc,
                                                    const uint32_t *plist, const uint32_t *grp,
@@ -308,11 +376,11 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, LineCols l
     auto eval = [&](r28::sp &sx, uint32_t j) {
       const uint32_t pair = pn, cj = cn;
       if (!g_prefetch) {
-        ml_eval28(sx, L, np, cj, P, Pc, pair, el);
+        ml_eval28<PCN>(sx, L, np, cj, P, Pc, pair, el);
         if (j + 1 < cnt) pn = plist[at + (j + 1) * stride], cn = colj(j + 1, pn);
         return;
       }
-      ml_eval28_reg(sx, lw, np, cj, P, Pc, pair);
+      ml_eval28_reg<PCN>(sx, lw, np, cj, P, Pc, pair);
       if (j + 1 < cnt) {
         pn = plist[at + (j + 1) * stride];
         cn = colj(j + 1, pn);
@@ -328,7 +396,10 @@ __global__ void __launch_bounds__(WG) k_ml_group28(const uint32_t *L, LineCols l
       r28::sp_mul_sp_lazy(acc, sa, sb);
       for (uint32_t j = 2; j < cnt; j++) {
         eval(sa, j);
-        r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
+        if constexpr (KARA)
+          r28::fe12_mul_034_kara_st(acc, sa, park + threadIdx.x, WG);
+        else
+          r28::fe12_mul_034_lazy_st(acc, sa, park + threadIdx.x, WG);
       }
     }
   }
@@ -409,13 +480,32 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
 }
 
 // the pairs' G1 points by line column (Pc word w of column col[pair] at w * ncol + col): the
-// Miller kernels' point loads coalesce like their line loads
+// Miller kernels' point loads coalesce like their line loads.  Each point is NORMALIZED on the
+// way (r06): g1s (x, y, c) = (xP c, yP c, c) becomes (2^8 xP, 2^8 yP, 1), i.e. x 2^8 / c and
+// y 2^8 / c with one inversion per pair (safegcd, bls_inv.h; ~40 products' worth per pair against
+// the 136 products per pair its 68 line evaluations save, see ml_eval28); infinity (c = 0) stays
+// all zero.  The 2^8 matches the engine-form reading of the line words (ml_eval28).
 __global__ void __launch_bounds__(WG) k_ml_pcols(const g1s *P, const uint32_t *col, uint32_t np,
                                                  uint32_t ncol, uint32_t *Pc) {
   const uint32_t pair = blockIdx.x * WG + threadIdx.x;
   if (pair >= np) return;
   const uint32_t c = col[pair];
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(P + pair);
+  g1s p = P[pair], o;
+  if (fp_is_zero(p.c)) {
+    fp_zero(o.x);
+    fp_zero(o.y);
+    fp_zero(o.c);
+  } else {
+    constexpr fp K8 = {{0x0347fcb8u, 0x19d80000u, 0x6d2002b1u, 0x12e00cdeu, 0xa2090c72u, 0x37669f83u,
+                        0xda0f73e0u, 0x09b09b42u, 0x8f1297bbu, 0xa7c515d9u, 0xfcfa012cu, 0x0577a659u}};  // 2^8 R
+    fp inv;
+    fp_inv(inv, p.c);
+    fp_mul(inv, inv, K8);  // 2^8 / c
+    fp_mul(o.x, p.x, inv);
+    fp_mul(o.y, p.y, inv);
+    fp_one(o.c);
+  }
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(&o);
 #pragma unroll
   for (int i = 0; i < 36; i++) Pc[(size_t)i * ncol + c] = w[i];
 }
@@ -432,10 +522,18 @@ void launch_ml_group(hipStream_t st, const uint32_t *lines, LineCols lc, uint32_
   if (g_ml_r28 && V28) {
     if (g_ml_dma)
       k_ml_group28<true, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else if (g_ml_kara && Pc)
+      k_ml_group28<false, false, true, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else if (g_ml_kara)
+      k_ml_group28<false, false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, nullptr, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else if (g_ml_prefetch && Pc)  // the points by column, normalized (k_ml_pcols): 4-product lines
+      k_ml_group28<false, true, false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     else if (g_ml_prefetch)
-      k_ml_group28<false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+      k_ml_group28<false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, nullptr, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else if (Pc)
+      k_ml_group28<false, false, false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     else
-      k_ml_group28<false, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+      k_ml_group28<false, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, nullptr, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     const uint32_t nvals = ngroup * (uint32_t)(e1 - e0);
     k_ml_pack28<<<nblk((size_t)nvals * 12), WG, 0, st>>>(V28, ngroup, e0, nvals, V0);
     return;

@@ -207,5 +207,46 @@ class MultiVerifier(Verifier):
             raise SignatureInvalid(SignatureKind.Multi)
         return None
 
+    def verify_each(self) -> List[bool]:
+        """f2 (r06, a new method of the drop-in's MultiVerifier): which collected sets verify ON
+        THEIR OWN, in ONE device submission (gbls_verify_batch_compressed: every set its own
+        check with Signature::verify / fast_aggregate_verify semantics -- the verdict the
+        singular path would reach).  A set whose signature does not decode is False.  For a
+        caller whose batch failed, so that only the failing items take the singular path
+        (split_failed_batch)."""
+        if not self.triples:
+            return []
+        outcomes = bls.Signature.verify_batch_compressed(
+            [t.message for t in self.triples], [t.signature_bytes for t in self.triples],
+            [t.keys() for t in self.triples])
+        return [status == 0 and ok for status, ok in outcomes]
+
     def has_option(self, option: VerifierOption) -> bool:
         return option in self.options
+
+
+def split_failed_batch(items: List, item_triples: List[Optional[List[Triple]]]):
+    """The drop-in's fallback after a failed gossip batch (rust/bls_patch/attestation_verifier.rs,
+    replacing /root/reference/p2p/src/attestation_verifier.rs:231-238 and 379-384, where every
+    item of the failed batch is re-verified one by one on the CPU).
+
+    item_triples[k]: the signature sets of item k IN ORDER (an attestation has one; an aggregate
+    three: selection proof, aggregate-and-proof signature, attestation), or None when they cannot
+    be built (the singular path then reports why).  One submission (MultiVerifier.verify_each)
+    decides every set; returns (passed, failing): the items whose sets all verify keep their batch
+    results, only the failing ones go to the singular path."""
+    if len(items) != len(item_triples):
+        raise ValueError("one triple list per item")
+    owner, triples = [], []
+    for k, ts in enumerate(item_triples):
+        for t in ts or []:
+            owner.append(k)
+            triples.append(t)
+    verified = MultiVerifier(triples=triples).verify_each()
+    bad = [ts is None for ts in item_triples]
+    for k, ok in zip(owner, verified):
+        if not ok:
+            bad[k] = True
+    passed = [it for it, b in zip(items, bad) if not b]
+    failing = [it for it, b in zip(items, bad) if b]
+    return passed, failing

@@ -174,9 +174,23 @@ pub fn available() -> bool {
 
 /// Engine layout of a blst public key: blst's affine point (its safe `From`), limbs copied.
 /// Both sides hold Montgomery limbs (R = 2^384) with all-zero infinity, so nothing is recomputed.
+#[cfg(not(feature = "serialized-points"))]
 #[must_use]
 pub fn p1_of_public_key(key: &RawPublicKey) -> P1 {
     let point = blst_p1_affine::from(key);
+    P1 { x: point.x.l, y: point.y.l }
+}
+
+/// Engine layout of a blst public key (feature `serialized-points`): its uncompressed
+/// serialisation decoded by blst's own decoder into the affine limbs (infinity -> all zero).
+#[cfg(feature = "serialized-points")]
+#[must_use]
+pub fn p1_of_public_key(key: &RawPublicKey) -> P1 {
+    let bytes = key.serialize();
+    let mut point = blst_p1_affine::default();
+    // SAFETY: `bytes` is a live 96-byte uncompressed encoding and `point` a valid output; a key
+    // of blst's own type always decodes (its status carries no information here).
+    let _status = unsafe { blst::blst_p1_deserialize(&mut point, bytes.as_ptr()) };
     P1 { x: point.x.l, y: point.y.l }
 }
 
@@ -191,9 +205,21 @@ pub fn public_key_of_p1(point: &P1) -> Result<RawPublicKey, BLST_ERROR> {
 }
 
 /// Engine layout of a blst signature (see [`p1_of_public_key`]).
+#[cfg(not(feature = "serialized-points"))]
 #[must_use]
 pub fn p2_of_signature(signature: &RawSignature) -> P2 {
     let point = blst_p2_affine::from(signature);
+    P2 { x: [point.x.fp[0].l, point.x.fp[1].l], y: [point.y.fp[0].l, point.y.fp[1].l] }
+}
+
+/// Engine layout of a blst signature (feature `serialized-points`, see [`p1_of_public_key`]).
+#[cfg(feature = "serialized-points")]
+#[must_use]
+pub fn p2_of_signature(signature: &RawSignature) -> P2 {
+    let bytes = signature.serialize();
+    let mut point = blst_p2_affine::default();
+    // SAFETY: `bytes` is a live 192-byte uncompressed encoding and `point` a valid output.
+    let _status = unsafe { blst::blst_p2_deserialize(&mut point, bytes.as_ptr()) };
     P2 { x: [point.x.fp[0].l, point.x.fp[1].l], y: [point.y.fp[0].l, point.y.fp[1].l] }
 }
 

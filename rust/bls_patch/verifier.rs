@@ -226,3 +226,25 @@ fn finish_on_cpu(&self) -> Result<()> {
 
     Ok(())
 }
+
+// ---------------------------------------------------------------- MultiVerifier::verify_each (f2)
+// A new public method of `impl MultiVerifier` (r06): which collected sets verify ON THEIR OWN, in
+// ONE engine submission (`gbls_verify_batch_compressed`: every set its own check with
+// `Signature::verify` / `fast_aggregate_verify` semantics -- the verdict the singular path would
+// reach -- coalesced with concurrent callers; from 2048 sets the engine groups 8 checks per
+// final exponentiation and re-checks failed groups' members on the device).  A set whose
+// signature does not decode is `false`.  For a caller whose batch failed, so that only the
+// failing items take its singular path (rust/bls_patch/attestation_verifier.rs, replacing the
+// per-item loops of p2p/src/attestation_verifier.rs:231-238,379-384).
+// `None`: no engine verdict (absent engine or engine error) -- the caller keeps the reference's
+// per-item fallback.
+
+#[must_use]
+pub fn verify_each(&self) -> Option<Vec<bool>> {
+    if self.triples.is_empty() {
+        return Some(Vec::new());
+    }
+    let (messages, signature_bytes, points, offsets) = engine_sets(&self.triples);
+    bls::gpu::verify_batch_compressed(&messages, &signature_bytes, &points, &offsets)
+        .map(|outcomes| outcomes.into_iter().map(|outcome| matches!(outcome, Ok(true))).collect())
+}

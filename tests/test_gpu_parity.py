@@ -230,7 +230,9 @@ def test_aggregate_segments_rows(L, G, B):
     sizes[5] = 0
     idx = rng.integers(0, nreg, size=int(sizes.sum()), dtype=np.uint32)
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
-    idx[int(offs[9])] = nreg + 3  # out of range in segment 9 (sizes[9] > 0 checked below)
+    # out of range in segment 9 (sizes[9] > 0 checked below): past the registry's current size,
+    # which earlier tests of the same process may have grown beyond nreg
+    idx[int(offs[9])] = max(nreg, L.gbls_registry_size()) + 3
     assert sizes[9] > 0
     ns = len(sizes)
     o_rows = ctypes.create_string_buffer(96 * ns)

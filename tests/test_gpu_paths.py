@@ -303,8 +303,8 @@ def test_bucket_msm_parity_subprocess():
     assert res["zero_scalar"] == 5
 
 
-@pytest.mark.parametrize("knobs", [["GBLS_ML_DMA=1"], ["GBLS_ML_R28=0"], ["GBLS_LANE_R28=0"]],
-                         ids=["ml-lds-dma", "ml-radix32", "lanes-radix32"])
+@pytest.mark.parametrize("knobs", [["GBLS_ML_DMA=1"], ["GBLS_ML_R28=0"], ["GBLS_LANE_R28=0"], ["GBLS_ML_KARA=1"]],
+                         ids=["ml-lds-dma", "ml-radix32", "lanes-radix32", "ml-karatsuba"])
 def test_kernel_variants_subprocess(knobs):
     """The non-default kernel forms an operator can select (k_ml_group28 with the line staged
     in LDS by DMA loads; the 32-bit-limb k_ml_group; the 32-bit-limb line / cofactor lanes):
