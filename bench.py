@@ -96,10 +96,12 @@ def cpu_threads():
 def pmc_traffic(kernel, default_cmd):
     """HBM bytes per launch of `kernel` (a stage name: k_ml_group is the radix-2^28
     k_ml_group28 of the default build) from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
-    summary of the default command's 16-batch launches (profiles/r05/z_c2_pmc_bytes.csv,
+    summary of the default command's 16-batch launches (profiles/r06/z_c2_pmc_bytes.csv,
     tools/prof/pmc_bytes.py --largest; FETCH_SIZE doubled per the gfx950 correction).  None for
     other commands or if absent."""
-    path = os.path.join(ROOT, "profiles", "r05", "z_c2_pmc_bytes.csv")
+    path = os.path.join(ROOT, "profiles", "r06", "z_c2_pmc_bytes.csv")
+    if not os.path.exists(path):  # the round's checkpoint pass until the final one is committed
+        path = os.path.join(ROOT, "profiles", "r06", "o_c2_pmc_bytes.csv")
     if not default_cmd or not os.path.exists(path):
         return None
     with open(path) as f:

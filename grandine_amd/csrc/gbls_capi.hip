@@ -494,6 +494,8 @@ struct Engine {
   // ... and normal requests do not start new submissions meanwhile (up to 4 ms, gbls_sched.h
   // Config::hold): the block shares the GPU only with the submissions already running
   bool block_hold = true;
+  bool lines_s_main = false;  // experiments: the MSM pairs' lines on the main stream after the join,
+  bool lines_s_lane = false;  // ... in the one-lane form
   std::atomic<int> block_active{0};
 } g;
 
@@ -583,6 +585,8 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_ML_DMA")) g_ml_dma = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_ML_PREFETCH")) g_ml_prefetch = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_ML_KARA")) g_ml_kara = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_LINES_S_MAIN")) g.lines_s_main = std::atoi(e) != 0;
+    if (const char *e = std::getenv("GBLS_LINES_S_LANE")) g.lines_s_lane = std::atoi(e) != 0;
   }
   int replicas = (int)(flags & 0xffu);
   if (replicas < 1) replicas = 1;
@@ -972,11 +976,14 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
                    c.P.as<g1s>(), c.H.as<g2a>(), seg_err, sj, c.ev_pks);
     }
   }
-  {  // the extra pairs' lines of the first event slice (all events when not sliced)
+  // experiment (GBLS_LINES_S_MAIN): the MSM's extra pairs' lines on the main stream after the
+  // join (high priority) instead of on the signature-side stream
+  const bool lines_s_main = msm && !sliced && g.lines_s_main;
+  if (!lines_s_main) {  // the extra pairs' lines of the first event slice (all events when not sliced)
     StageTimer t(S_LINES_S, side2);
     if (!sj || !launch_lines_jac(side2, sj, 1, N, NS, lc, c.lines.as<uint32_t>()))
       launch_lines(side2, c.H.as<g2a>(), N, (uint32_t)(nseg * X), lc, 0, EC, c.Ts.as<g2h>(),
-                   c.lines.as<uint32_t>());
+                   c.lines.as<uint32_t>(), g.lines_s_lane);
   }
   // latency regime: H(m) stays Jacobian (over Q[2 i]) and its lines take it projectively,
   // no inversion on the main chain
@@ -995,6 +1002,11 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
   HIPCHK(hipEventRecord(c.ev_side2, side2));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side1, 0));
   HIPCHK(hipStreamWaitEvent(st, c.ev_side2, 0));
+  if (lines_s_main) {
+    StageTimer t(S_LINES_S, st);
+    launch_lines(st, c.H.as<g2a>(), N, (uint32_t)(nseg * X), lc, 0, EC, c.Ts.as<g2h>(), c.lines.as<uint32_t>(),
+                 g.lines_s_lane);
+  }
   const uint32_t *Pc = nullptr;  // the points by line column (radix-2^28 Miller kernel)
   if (g_ml_r28 && mt.ngp) {
     launch_ml_pcols(st, c.P.as<g1s>(), lc.col, NP, lc.ncol, c.Pc.as<uint32_t>());

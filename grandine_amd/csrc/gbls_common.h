@@ -142,7 +142,7 @@ struct LineCols {
 // lines of events [e0, e1) of pairs [first, first + count) (H indexed by pair), stored at
 // event e - e0; Ts: the running point between event slices (null: full range)
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, LineCols lc,
-                  int e0, int e1, g2h *Ts, uint32_t *lines);
+                  int e0, int e1, g2h *Ts, uint32_t *lines, bool lane = false);
 // all events of pairs [first, first + count) from Jacobian points Qj[stride i] (count <=
 // kW4Max, else false)
 bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t first, uint32_t count,

@@ -394,8 +394,12 @@ bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t f
 }
 
 void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, LineCols lc,
-                  int e0, int e1, g2h *Ts, uint32_t *lines) {
+                  int e0, int e1, g2h *Ts, uint32_t *lines, bool lane) {
   if (!count) return;
+  if (lane && g_lane_r28) {  // the caller asks for the one-lane form (fewest instructions per pair)
+    k_lines_lane28<<<nblk(count), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);
+    return;
+  }
   if (count <= kW4Max)
     (count <= w4::kExclusiveMaxWaves ? k_lines_w4<true> : k_lines_w4<false>)<<<count, 64, 0, st>>>(
         H, first, count, lc, e0, e1, Ts, lines);
