@@ -276,6 +276,33 @@ class Signature:
             None, G.u32_array(off), G.u64_array(randoms), n, st, call_flags)
 
     @staticmethod
+    def multi_verify_compressed_indexed(messages: Iterable[bytes], signature_bytes: Iterable[bytes],
+                                        validator_indices: Iterable[Sequence[int]], randoms: Sequence[int] = None,
+                                        call_flags: int = 0) -> int:
+        """multi_verify_compressed with each set's keys named by REGISTRY INDICES (f1: the engine
+        gathers and sums the registry's keys on the device; 4 bytes per key instead of 96).
+        Returns as multi_verify_compressed; an index past the registry fails its set."""
+        msgs = [bytes(m) for m in messages]
+        sigs = [bytes(s) for s in signature_bytes]
+        idx = [list(v) for v in validator_indices]
+        n = len(sigs)
+        if n == 0 or len(msgs) != n or len(idx) != n:
+            return G.VERIFY_FAIL
+        if any(len(m) != 32 for m in msgs) or any(len(s) != 96 for s in sigs):
+            raise ValueError("messages must be 32-byte signing roots and signatures 96 bytes")
+        if randoms is None:
+            randoms = [secrets.randbits(64) or 1 for _ in range(n)]
+        off = [0]
+        for v in idx:
+            off.append(off[-1] + len(v))
+        flat = [i for v in idx for i in v]
+        L = G.lib()
+        st = G.i32_array(n)
+        return L.gbls_multi_verify_compressed_ex(
+            G.buf(b"".join(msgs)), G.buf(b"".join(sigs)), None, G.u32_array(flat or [0]), G.u32_array(off),
+            G.u64_array(randoms), n, st, call_flags)
+
+    @staticmethod
     def verify_batch_compressed(messages: Iterable[bytes], signature_bytes: Iterable[bytes],
                                 public_keys: Iterable) -> List:
         """SingleVerifier::extend's try_from + verify per triple (verifier.rs:215-236) as ONE
@@ -372,3 +399,38 @@ def public_keys_batch(secret_keys: Sequence[bytes]) -> List[PublicKey]:
     out = ctypes.create_string_buffer(96 * max(n, 1))
     G.check(L.gbls_sk_to_pk(G.buf(b"".join(secret_keys)), n, out), "gbls_sk_to_pk")
     return [PublicKey(out.raw[96 * i:96 * (i + 1)]) for i in range(n)]
+
+
+class Registry:
+    """Mirror of ``bls::gpu::registry`` (rust/bls_patch/gpu.rs, f1): the engine's device-resident
+    copy of a FINALIZED validator list (indices name the same key on every fork only up to the
+    finalized state).  ``mirror_finalized`` loads the new tail of the list with one
+    gbls_registry_set; ``covers`` says whether a batch may name registry slots instead of key
+    points."""
+
+    _mirrored = 0
+
+    @classmethod
+    def mirror_finalized(cls, keys: Sequence[bytes]) -> int:
+        n = len(keys) - cls._mirrored
+        if n <= 0:
+            return cls._mirrored
+        tail = b"".join(bytes(k) for k in keys[cls._mirrored:])
+        L = G.lib()
+        st = G.i32_array(n)
+        G.check(L.gbls_registry_set(cls._mirrored, G.buf(tail), n, st), "gbls_registry_set")
+        cls._mirrored = len(keys)
+        return cls._mirrored
+
+    @classmethod
+    def mirrored(cls) -> int:
+        return cls._mirrored
+
+    @classmethod
+    def covers(cls, indices: Iterable[int]) -> bool:
+        return all(0 <= int(i) < cls._mirrored for i in indices)
+
+    @classmethod
+    def forget(cls) -> None:
+        """Tests: the process's engine registry was overwritten by someone else."""
+        cls._mirrored = 0

@@ -58,7 +58,7 @@ class Triple:
     ``verify_aggregate``, the message, signature and the KEY LIST whose sum is the key."""
 
     IS_NULL = False
-    __slots__ = ("message", "signature_bytes", "_key", "deferred")
+    __slots__ = ("message", "signature_bytes", "_key", "deferred", "indices")
 
     def __init__(self, message: bytes = bytes(32), signature_bytes: bytes = None,
                  public_key: "bls.PublicKey" = None):
@@ -66,6 +66,7 @@ class Triple:
         self.signature_bytes = bls.SignatureBytes(signature_bytes if signature_bytes is not None else bytes(96))
         self._key = public_key if public_key is not None else bls.PublicKey.default()
         self.deferred = None  # list of keys once verify_aggregate has run
+        self.indices = None   # their validator indices (verify_aggregate_indexed, f1)
 
     def verify_aggregate(self, message, signature_bytes, public_keys, signature_kind=None):
         """verifier.rs:387-405 without the reduce: the keys are kept and summed on the device by
@@ -75,6 +76,13 @@ class Triple:
         self.signature_bytes = bls.SignatureBytes(bytes(signature_bytes))
         self._key = bls.PublicKey.default()
         self.deferred = list(public_keys)
+
+    def verify_aggregate_indexed(self, message, signature_bytes, validator_indices, public_keys,
+                                 signature_kind=None):
+        """f1 (r06): verify_aggregate that also keeps the keys' validator indices
+        (rust/bls_patch/verifier.rs), so MultiVerifier.finish can name registry slots."""
+        self.verify_aggregate(message, signature_bytes, public_keys, signature_kind)
+        self.indices = [int(i) for i in validator_indices]
 
     @property
     def public_key(self) -> "bls.PublicKey":
@@ -174,6 +182,7 @@ class MultiVerifier(Verifier):
     def __init__(self, options: Iterable[VerifierOption] = (), triples: Optional[List[Triple]] = None):
         self.triples: List[Triple] = list(triples or [])
         self.options = set(options)
+        self.last_path = None  # "indices" or "points": the key form of the last finish (tests)
 
     @classmethod
     def from_triples(cls, triples: List[Triple]) -> "MultiVerifier":  # From<Vec<Triple>>
@@ -191,16 +200,29 @@ class MultiVerifier(Verifier):
     def extend(self, triples, signature_kind):
         self.triples.extend(triples)
 
+    def verify_aggregate_indexed(self, message, signature_bytes, validator_indices, public_keys, signature_kind):
+        t = Triple()
+        t.verify_aggregate_indexed(message, signature_bytes, validator_indices, public_keys, signature_kind)
+        self.triples.append(t)
+
     def finish(self, randoms=None):
         """verifier.rs:301-323."""
         if not self.triples:
             return None
         # decompression (verifier.rs:309-313) and multi_verify in one device submission
-        # key sums of deferred triples (Triple.verify_aggregate) on the device, same submission
-        rc = bls.Signature.multi_verify_compressed([t.message for t in self.triples],
-                                                   [t.signature_bytes for t in self.triples],
-                                                   [t.keys() for t in self.triples], randoms,
-                                                   0x1 if VerifierOption.BlockImport in self.options else 0)
+        # key sums of deferred triples (Triple.verify_aggregate) on the device, same submission;
+        # f1: registry indices instead of key points when every set has them and the engine's
+        # registry mirrors those validators (bls.Registry)
+        flags = 0x1 if VerifierOption.BlockImport in self.options else 0
+        msgs = [t.message for t in self.triples]
+        sigs = [t.signature_bytes for t in self.triples]
+        if all(t.indices is not None and bls.Registry.covers(t.indices) for t in self.triples):
+            self.last_path = "indices"
+            rc = bls.Signature.multi_verify_compressed_indexed(msgs, sigs, [t.indices for t in self.triples],
+                                                               randoms, flags)
+        else:
+            self.last_path = "points"
+            rc = bls.Signature.multi_verify_compressed(msgs, sigs, [t.keys() for t in self.triples], randoms, flags)
         if rc not in (0, 5):
             raise bls.DecompressionFailed(rc)
         if rc != 0:

@@ -412,6 +412,75 @@ pub fn verify_batch_compressed(
     Ok(statuses.into_iter().zip(verdicts).map(|(s, v)| outcome(s, v)).collect())
 }
 
+/// f1: loads compressed public keys at registry slots `first ..` (decompressed and validated once
+/// on the device, replicated to every engine device).  Per key: `Ok(())`, or the decoder's
+/// BLST_ERROR (that slot stays empty and a set naming it fails).
+pub fn registry_set(first: usize, keys: &[[u8; 48]]) -> EngineResult<Vec<Result<(), BLST_ERROR>>> {
+    let mut statuses = vec![ffi::GBLS_BAD_ENCODING; keys.len()];
+    // SAFETY: `keys` is a live slice of keys.len() 48-byte entries and `statuses` as many slots.
+    let rc = unsafe { ffi::gbls_registry_set(first, keys.as_ptr(), keys.len(), statuses.as_mut_ptr()) };
+    status(rc)?;
+    Ok(statuses.into_iter().map(|s| if s == ffi::GBLS_SUCCESS { Ok(()) } else { Err(blst_error(s)) }).collect())
+}
+
+/// f1: the number of registry slots loaded (0 before any `registry_set`).
+#[must_use]
+pub fn registry_size() -> usize {
+    // SAFETY: no arguments; the library guards its registry with its own lock.
+    unsafe { ffi::gbls_registry_size() }
+}
+
+/// a2 + f1: `MultiVerifier::finish` as one submission with REGISTRY INDICES: set i's key is the
+/// sum of the registry keys `indices[index_offsets[i] .. index_offsets[i + 1]]` (gathered and
+/// summed on the device), signatures as 96-byte encodings decompressed in the same submission.
+/// `Ok(Err(e))`: the first signature that does not decode; `Ok(Ok(v))`: the verdict.  An index
+/// past the registry fails its set (a verdict, not an error).
+pub fn multi_verify_compressed_indexed(
+    messages: &[[u8; 32]],
+    signatures: &[[u8; 96]],
+    indices: &[u32],
+    index_offsets: &[u32],
+    scalars: &[u64],
+    class: CallClass,
+) -> EngineResult<Result<bool, BLST_ERROR>> {
+    let n = messages.len();
+    let ranges_ok = index_offsets.len() == n + 1
+        && index_offsets.first() == Some(&0)
+        && index_offsets.windows(2).all(|w| w[0] <= w[1])
+        && usize::try_from(index_offsets[n]).is_ok_and(|last| last == indices.len());
+    if n == 0 || signatures.len() != n || scalars.len() != n || scalars.contains(&0) || !ranges_ok {
+        return Err(EngineError::Argument);
+    }
+    let mut statuses = vec![ffi::GBLS_BAD_ENCODING; n];
+    let flags = match class {
+        CallClass::Normal => 0,
+        CallClass::BlockImport => ffi::GBLS_CALL_BLOCK,
+    };
+    // SAFETY: live slices of n elements each, `indices` of index_offsets[n] entries and
+    // `index_offsets` of n + 1 (checked above); no key points.
+    let rc = unsafe {
+        ffi::gbls_multi_verify_compressed_ex(
+            messages.as_ptr(),
+            signatures.as_ptr(),
+            ptr::null(),
+            indices.as_ptr(),
+            index_offsets.as_ptr(),
+            scalars.as_ptr(),
+            n,
+            statuses.as_mut_ptr(),
+            flags,
+        )
+    };
+    if let Some(e) = last_error() {
+        return Err(e);
+    }
+    Ok(match rc {
+        ffi::GBLS_SUCCESS => Ok(true),
+        ffi::GBLS_VERIFY_FAIL => Ok(false),
+        decode => Err(blst_error(decode)),
+    })
+}
+
 /// f2: per-set verdicts of a batch (`true` = the set verifies on its own).
 pub fn multi_verify_bisect(
     messages: &[[u8; 32]],

@@ -129,3 +129,65 @@ fn counted<T>(call: impl FnOnce() -> Result<T, EngineError>) -> Option<T> {
     }
     result.ok()
 }
+
+/// `MultiVerifier::finish` with registry indices (f1): as [`multi_verify_compressed`], set i's key
+/// the sum of the registry keys `indices[index_offsets[i] .. index_offsets[i + 1]]`.
+#[must_use]
+pub fn multi_verify_compressed_indexed(
+    messages: &[[u8; 32]],
+    signature_bytes: &[[u8; 96]],
+    indices: &[u32],
+    index_offsets: &[u32],
+    scalars: &[u64],
+    class: CallClass,
+) -> Option<Result<bool, blst::BLST_ERROR>> {
+    counted(|| {
+        bls_gpu_sys::multi_verify_compressed_indexed(messages, signature_bytes, indices, index_offsets, scalars, class)
+    })
+}
+
+/// f1: the engine's copy of the validator registry (device-resident keys, decompressed once).
+///
+/// Validator indices name the same key on every fork only up to the finalized state: a deposit
+/// processed on two branches can give one index two keys.  So the node mirrors the FINALIZED
+/// state's validators (`mirror_finalized`, called where finalization advances and for the anchor
+/// state at start-up), and a batch goes to the engine by indices only when every
+/// index it names is below the mirrored length (`covers`); otherwise it keeps the key points.
+pub mod registry {
+    use std::sync::Mutex;
+
+    use crate::PublicKeyBytes;
+
+    /// validators loaded into the engine (a prefix of the finalized validator list)
+    static MIRRORED: Mutex<usize> = Mutex::new(0);
+
+    /// Loads validators `[mirrored, keys.len())` of a finalized state's validator list into the
+    /// engine's registry (one `gbls_registry_set` for the new tail) and returns the mirrored
+    /// length.  Keys never change once a validator is finalized, so the prefix already loaded is
+    /// not sent again.  A key that does not decode leaves its slot empty (sets naming it fail,
+    /// as `CachedPublicKey::decompress` would fail them).  Without an engine: 0.
+    pub fn mirror_finalized(keys: &[PublicKeyBytes]) -> usize {
+        let mut mirrored = MIRRORED.lock().unwrap_or_else(std::sync::PoisonError::into_inner);
+        if !super::available() || keys.len() <= *mirrored {
+            return *mirrored;
+        }
+        let tail = keys[*mirrored..].iter().map(|bytes| bytes.to_fixed_bytes()).collect::<Vec<[u8; 48]>>();
+        if bls_gpu_sys::registry_set(*mirrored, &tail).is_ok() {
+            *mirrored = keys.len();
+        }
+        *mirrored
+    }
+
+    /// The mirrored length (validators whose keys the engine resolves by index).
+    #[must_use]
+    pub fn mirrored() -> usize {
+        *MIRRORED.lock().unwrap_or_else(std::sync::PoisonError::into_inner)
+    }
+
+    /// `true` when every index is below the mirrored length.
+    #[must_use]
+    pub fn covers(indices: &[u32]) -> bool {
+        let mirrored = mirrored();
+        indices.iter().all(|&index| usize::try_from(index).is_ok_and(|index| index < mirrored))
+    }
+}

@@ -30,10 +30,25 @@
 //   which the block paths pass when they build their verifier
 //   (p2p/src/block_verification_pool.rs:109, fork_choice_control/src/tasks.rs:101).
 //
+// * f1 (r06): the `Verifier` trait gains one provided method, added at verifier.rs:16-69 and
+//   forwarded by `impl<V: Verifier> Verifier for &mut V` (verifier.rs:73-119):
+//
+//       fn verify_aggregate_indexed<'keys>(&mut self, message: H256, signature_bytes: SignatureBytes,
+//           validator_indices: &[ValidatorIndex],
+//           public_keys: impl IntoIterator<IntoIter = impl Iterator<Item = &'keys PublicKey> + Send>,
+//           signature_kind: SignatureKind) -> Result<()> {
+//           self.verify_aggregate(message, signature_bytes, public_keys, signature_kind)
+//       }
+//
+//   `Triple` and `MultiVerifier` override it to keep the indices; the attestation predicate calls
+//   it (rust/bls_patch/predicates.rs).  `finish` then names registry slots (4 bytes per key)
+//   instead of 96-byte points when the engine mirrors those validators (bls::gpu::registry).
+//
 // Without an engine verdict (no device, engine error) each body runs the reference's blst code,
 // with the deferred sums formed by blst first (`Triple::public_key`).
 
-/// verifier.rs:349-354, plus the deferred key list of `verify_aggregate`.
+/// verifier.rs:349-354, plus the deferred key list of `verify_aggregate` and, when the caller
+/// knows them, the keys' validator indices (f1, `verify_aggregate_indexed`).
 #[derive(Default)]
 pub struct Triple {
     message: H256,
@@ -41,6 +56,9 @@ pub struct Triple {
     public_key: PublicKey,
     // Some(keys): the public key is the sum of `keys` (Triple::verify_aggregate), not yet formed
     deferred: Option<Vec<PublicKey>>,
+    // Some(indices): the deferred keys are these validators' (the engine's registry can resolve
+    // them on the device, bls::gpu::registry)
+    indices: Option<Vec<u32>>,
 }
 
 assert_not_impl_any!(Triple: Copy);
@@ -49,7 +67,7 @@ impl Triple {
     /// The reference's `derive(Constructor)` (verifier.rs:349): one resolved key.
     #[must_use]
     pub const fn new(message: H256, signature_bytes: SignatureBytes, public_key: PublicKey) -> Self {
-        Self { message, signature_bytes, public_key, deferred: None }
+        Self { message, signature_bytes, public_key, deferred: None, indices: None }
     }
 
     /// The set's key for the blst bodies: the deferred sum formed now (reference reduce, identity
@@ -68,6 +86,20 @@ impl Triple {
             None => points.push(bls::gpu::public_key_point(&self.public_key)),
         }
     }
+}
+
+/// Registry arguments of a run of triples (f1): every set's validator indices and per-set offsets,
+/// or `None` when some set has no indices or names a validator the engine's registry does not
+/// mirror (the caller then ships key points, engine_sets).
+fn engine_indices(triples: &[Triple]) -> Option<(Vec<u32>, Vec<u32>)> {
+    let mut indices = Vec::new();
+    let mut offsets = Vec::with_capacity(triples.len() + 1);
+    offsets.push(0);
+    for triple in triples {
+        indices.extend_from_slice(triple.indices.as_deref()?);
+        offsets.push(u32::try_from(indices.len()).ok()?);
+    }
+    bls::gpu::registry::covers(&indices).then_some((indices, offsets))
 }
 
 /// Engine arguments of a run of triples: 32-byte messages, 96-byte signatures, key points and
@@ -116,7 +148,26 @@ impl Verifier for Triple {
         _signature_kind: SignatureKind,
     ) -> Result<()> {
         let keys = public_keys.into_iter().copied().collect_vec();
-        *self = Self { message, signature_bytes, public_key: PublicKey::default(), deferred: Some(keys) };
+        *self = Self { message, signature_bytes, public_key: PublicKey::default(), deferred: Some(keys), indices: None };
+        Ok(())
+    }
+
+    /// f1 (r06): `verify_aggregate` that also keeps the keys' validator indices, so that
+    /// `MultiVerifier::finish` can name registry slots instead of shipping 96-byte points when the
+    /// engine's registry mirrors those validators (bls::gpu::registry::covers).  The keys are kept
+    /// as well: the points path and the blst fallback use them.
+    #[inline]
+    fn verify_aggregate_indexed<'keys>(
+        &mut self,
+        message: H256,
+        signature_bytes: SignatureBytes,
+        validator_indices: &[ValidatorIndex],
+        public_keys: impl IntoIterator<IntoIter = impl Iterator<Item = &'keys PublicKey> + Send>,
+        signature_kind: SignatureKind,
+    ) -> Result<()> {
+        self.verify_aggregate(message, signature_bytes, public_keys, signature_kind)?;
+        // an index past u32 (no such validator set exists) keeps the points path
+        self.indices = validator_indices.iter().map(|&index| u32::try_from(index).ok()).collect();
         Ok(())
     }
 
@@ -173,6 +224,24 @@ fn extend_on_cpu(triples: &[Triple], signature_kind: SignatureKind) -> Result<()
     Ok(())
 }
 
+// ---------------------------------------------------------------- MultiVerifier::verify_aggregate_indexed
+// (f1, r06; in `impl Verifier for MultiVerifier` next to verify_aggregate, verifier.rs:275-287)
+
+#[inline]
+fn verify_aggregate_indexed<'keys>(
+    &mut self,
+    message: H256,
+    signature_bytes: SignatureBytes,
+    validator_indices: &[ValidatorIndex],
+    public_keys: impl IntoIterator<IntoIter = impl Iterator<Item = &'keys PublicKey> + Send>,
+    signature_kind: SignatureKind,
+) -> Result<()> {
+    let mut triple = Triple::default();
+    triple.verify_aggregate_indexed(message, signature_bytes, validator_indices, public_keys, signature_kind)?;
+    self.triples.push(triple);
+    Ok(())
+}
+
 // ---------------------------------------------------------------- MultiVerifier::finish
 
 #[inline]
@@ -196,7 +265,21 @@ fn finish(&self) -> Result<()> {
         bls::gpu::CallClass::Normal
     };
 
-    match bls::gpu::multi_verify_compressed(&messages, &signature_bytes, &points, &offsets, &randoms, class) {
+    // f1: registry indices (4 bytes per key, resolved on the device) when every set has them and
+    // the registry mirrors those validators; else the key points
+    let verdict = match engine_indices(&self.triples) {
+        Some((indices, index_offsets)) => bls::gpu::multi_verify_compressed_indexed(
+            &messages,
+            &signature_bytes,
+            &indices,
+            &index_offsets,
+            &randoms,
+            class,
+        ),
+        None => bls::gpu::multi_verify_compressed(&messages, &signature_bytes, &points, &offsets, &randoms, class),
+    };
+
+    match verdict {
         Some(verdict) => {
             let verdict = verdict.map_err(bls::Error::DecompressionFailed)?;
             ensure!(verdict, Error::SignatureInvalid(SignatureKind::Multi));

@@ -318,3 +318,35 @@ def test_gossip_fallback_names_failing_items_in_one_submission():
     assert "engine_sets(&self.triples)" in ve
     assert "bls::gpu::verify_batch_compressed(&messages, &signature_bytes, &points, &offsets)" in ve
     assert "matches!(outcome, Ok(true))" in ve
+
+
+def test_registry_mirror_names_slots_in_finish():
+    """VERDICT r05 "next 4" (f1 as code): the attestation predicate passes the attesting indices
+    (verify_aggregate_indexed), Triple keeps them beside the keys, finish names registry slots
+    only when every set has indices and the registry mirrors them (else the key points), the
+    mirror loads only a finalized validator list's new tail, and the sys crate's indexed wrapper
+    passes indices + offsets with no key points."""
+    pred = _strip_comments(open(os.path.join(PATCH, "predicates.rs")).read())
+    assert "verifier.verify_aggregate_indexed(" in pred and "&validator_indices," in pred
+    assert "accessors::public_key(state, validator_index)?" in pred and ".decompress()" in pred
+    ver = _strip_comments(open(os.path.join(PATCH, "verifier.rs")).read())
+    assert "indices: Option<Vec<u32>>," in ver
+    tvai = ver.split("fn verify_aggregate_indexed<'keys>(", 1)[1].split("\n    }", 1)[0]
+    assert "self.verify_aggregate(message, signature_bytes, public_keys, signature_kind)?;" in tvai
+    assert "u32::try_from(index).ok()" in tvai
+    ei = ver.split("fn engine_indices(", 1)[1].split("\n}", 1)[0]
+    assert "triple.indices.as_deref()?" in ei and "bls::gpu::registry::covers(&indices)" in ei
+    fin = ver.rsplit("fn finish(", 1)[1].split("\nfn ", 1)[0]
+    assert "match engine_indices(&self.triples)" in fin
+    assert "bls::gpu::multi_verify_compressed_indexed(" in fin and "bls::gpu::multi_verify_compressed(" in fin
+    assert "None => self.finish_on_cpu()" in fin
+    gpu = _strip_comments(open(os.path.join(PATCH, "gpu.rs")).read())
+    reg = gpu.split("pub mod registry {", 1)[1]
+    assert "keys[*mirrored..]" in reg and "bls_gpu_sys::registry_set(*mirrored, &tail)" in reg
+    assert "index < mirrored" in reg
+    fns = _rust_fns(open(SAFE).read())
+    body = fns["multi_verify_compressed_indexed"]
+    m = re.search(r"ffi::gbls_multi_verify_compressed_ex\((.*?)\)\s*\};", body, flags=re.S)
+    args = [a.strip() for a in m.group(1).split(",") if a.strip()]
+    assert args[2] == "ptr::null()" and args[3] == "indices.as_ptr()" and args[4] == "index_offsets.as_ptr()"
+    assert "status(rc)?" in fns["registry_set"] and "ffi::gbls_registry_set(first, keys.as_ptr()" in fns["registry_set"]
