@@ -71,6 +71,8 @@ constexpr size_t kShardMinSets = 1024;     // per device, before a batch is spli
 // 4.20-4.35M; and creating contexts inside a timed loop costs C4 a third (350-390k).
 // Block-import contexts are created by the first block import.
 constexpr int kPrewarmCtx[2] = {2, 0};
+// submissions of at least this many Miller pairs read normalized points (k_ml_pcols)
+constexpr uint32_t kPcnMinPairs = 32768;
 
 thread_local int t_last_error = GBLS_ERR_NONE;
 
@@ -494,6 +496,7 @@ struct Engine {
   // ... and normal requests do not start new submissions meanwhile (up to 4 ms, gbls_sched.h
   // Config::hold): the block shares the GPU only with the submissions already running
   bool block_hold = true;
+  bool ml_pcn = true;         // the Miller kernel reads normalized points by column (GBLS_ML_PCN)
   bool lines_s_main = false;  // experiments: the MSM pairs' lines on the main stream after the join,
   bool lines_s_lane = false;  // ... in the one-lane form
   std::atomic<int> block_active{0};
@@ -586,6 +589,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_ML_PREFETCH")) g_ml_prefetch = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_ML_KARA")) g_ml_kara = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LINES_S_MAIN")) g.lines_s_main = std::atoi(e) != 0;
+    if (const char *e = std::getenv("GBLS_ML_PCN")) g.ml_pcn = std::atoi(e) != 0;
     if (const char *e = std::getenv("GBLS_LINES_S_LANE")) g.lines_s_lane = std::atoi(e) != 0;
   }
   int replicas = (int)(flags & 0xffu);
@@ -1008,9 +1012,16 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
                  g.lines_s_lane);
   }
   const uint32_t *Pc = nullptr;  // the points by line column (radix-2^28 Miller kernel)
+  bool pcn = false;              // ... normalized
+  // Points by line column for the radix-2^28 Miller kernel: normalized (x 2^8 / c, y 2^8 / c, one
+  // inversion per pair, 4-product line evaluations) in the throughput regime; below it (blocks,
+  // gossip, single batches, C3's grouped checks) the inversion's latency sits on the critical
+  // path between the join and the Miller product, so the points keep their (x, y, c) form there
   if (g_ml_r28 && mt.ngp) {
-    launch_ml_pcols(st, c.P.as<g1s>(), lc.col, NP, lc.ncol, c.Pc.as<uint32_t>());
+    const bool normalize = g.ml_pcn && NP >= kPcnMinPairs;
+    launch_ml_pcols(st, c.P.as<g1s>(), lc.col, NP, lc.ncol, c.Pc.as<uint32_t>(), normalize);
     Pc = c.Pc.as<uint32_t>();
+    pcn = normalize;
   }
   for (int e0 = 0; e0 < ML_EVENTS; e0 += EC) {
     const int e1 = std::min(ML_EVENTS, e0 + EC);
@@ -1020,7 +1031,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
     }
     StageTimer t(S_ML_LEAF, st);
     launch_ml_group(st, c.lines.as<uint32_t>(), lc, mt.ngp, c.P.as<g1s>(), Pc, T + mt.plist_off,
-                    T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>(), c.V28.as<uint32_t>());
+                    T + mt.grp_off, (uint32_t)mt.ngroup, e0, e1, c.V0.as<fp12>(), c.V28.as<uint32_t>(), pcn);
   }
   ml_tail(c, st, mt, T, (uint32_t)nms, partials, n <= kSplitHornerMaxSets);
   if (st != caller) {

@@ -155,10 +155,10 @@ bool launch_lines_jac(hipStream_t st, const g2j *Qj, uint32_t stride, uint32_t f
 // Pc (nullable): the points by line column (launch_ml_pcols), read by the radix-2^28 kernel
 void launch_ml_group(hipStream_t st, const uint32_t *lines, LineCols lc, uint32_t ngp, const g1s *P,
                      const uint32_t *Pc, const uint32_t *plist, const uint32_t *groups, uint32_t ngroup,
-                     int e0, int e1, fp12 *V0, uint32_t *V28);
+                     int e0, int e1, fp12 *V0, uint32_t *V28, bool pcn = false);
 // Pc[w * ncol + col[pair]] = word w of P[pair] (36 words per point), pairs [0, np)
 void launch_ml_pcols(hipStream_t st, const g1s *P, const uint32_t *col, uint32_t np, uint32_t ncol,
-                     uint32_t *Pc);
+                     uint32_t *Pc, bool normalize);
 void launch_ml_reduce(hipStream_t st, const fp12 *Vin, uint32_t nin, const uint32_t *red,
                       uint32_t nout, fp12 *Vout);
 // lim (device count, optional): only segments s with base + s < *lim run (the others exit)

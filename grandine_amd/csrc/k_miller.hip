@@ -485,13 +485,16 @@ __global__ void __launch_bounds__(64) k_ml_horner(const fp12 *V, uint32_t nseg, 
 // y 2^8 / c with one inversion per pair (safegcd, bls_inv.h; ~40 products' worth per pair against
 // the 136 products per pair its 68 line evaluations save, see ml_eval28); infinity (c = 0) stays
 // all zero.  The 2^8 matches the engine-form reading of the line words (ml_eval28).
+template <bool NORM>
 __global__ void __launch_bounds__(WG) k_ml_pcols(const g1s *P, const uint32_t *col, uint32_t np,
                                                  uint32_t ncol, uint32_t *Pc) {
   const uint32_t pair = blockIdx.x * WG + threadIdx.x;
   if (pair >= np) return;
   const uint32_t c = col[pair];
   g1s p = P[pair], o;
-  if (fp_is_zero(p.c)) {
+  if (!NORM) {  // the (x, y, c) form as it is
+    o = p;
+  } else if (fp_is_zero(p.c)) {
     fp_zero(o.x);
     fp_zero(o.y);
     fp_zero(o.c);
@@ -510,30 +513,34 @@ __global__ void __launch_bounds__(WG) k_ml_pcols(const g1s *P, const uint32_t *c
   for (int i = 0; i < 36; i++) Pc[(size_t)i * ncol + c] = w[i];
 }
 void launch_ml_pcols(hipStream_t st, const g1s *P, const uint32_t *col, uint32_t np, uint32_t ncol,
-                     uint32_t *Pc) {
-  if (np) k_ml_pcols<<<nblk(np), WG, 0, st>>>(P, col, np, ncol, Pc);
+                     uint32_t *Pc, bool normalize) {
+  if (!np) return;
+  if (normalize)
+    k_ml_pcols<true><<<nblk(np), WG, 0, st>>>(P, col, np, ncol, Pc);
+  else
+    k_ml_pcols<false><<<nblk(np), WG, 0, st>>>(P, col, np, ncol, Pc);
 }
 void launch_ml_group(hipStream_t st, const uint32_t *lines, LineCols lc, uint32_t ngp, const g1s *P,
                      const uint32_t *Pc, const uint32_t *plist, const uint32_t *groups, uint32_t ngroup, int e0,
-                     int e1, fp12 *V0, uint32_t *V28) {
+                     int e1, fp12 *V0, uint32_t *V28, bool pcn) {
   dim3 grid(nblk(ngroup), e1 - e0);
   if (!ngroup || e1 <= e0) return;
   const dim3 grid1(nblk(ngroup) * (uint32_t)(e1 - e0));
   if (g_ml_r28 && V28) {
     if (g_ml_dma)
       k_ml_group28<true, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
-    else if (g_ml_kara && Pc)
+    else if (g_ml_kara && pcn)
       k_ml_group28<false, false, true, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     else if (g_ml_kara)
-      k_ml_group28<false, false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, nullptr, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
-    else if (g_ml_prefetch && Pc)  // the points by column, normalized (k_ml_pcols): 4-product lines
+      k_ml_group28<false, false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else if (g_ml_prefetch && pcn)  // the points by column, normalized (k_ml_pcols): 4-product lines
       k_ml_group28<false, true, false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     else if (g_ml_prefetch)
-      k_ml_group28<false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, nullptr, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
-    else if (Pc)
+      k_ml_group28<false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+    else if (pcn)
       k_ml_group28<false, false, false, true><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     else
-      k_ml_group28<false, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, nullptr, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
+      k_ml_group28<false, false><<<grid1, WG, 0, st>>>(lines, lc, ngp, P, Pc, plist, groups, ngroup, e0, e1 - e0, (int)g_ml_xcd, V28);
     const uint32_t nvals = ngroup * (uint32_t)(e1 - e0);
     k_ml_pack28<<<nblk((size_t)nvals * 12), WG, 0, st>>>(V28, ngroup, e0, nvals, V0);
     return;
