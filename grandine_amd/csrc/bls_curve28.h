@@ -2,9 +2,11 @@
 // (DESIGN.md section 8's migration order): the engine's Jacobian formulas
 // (bls_curve.h jac_dbl / jac_add / mul_by_xabs, templates over the coordinate field) are
 // instantiated for r28::fe2 through the overload set below, found by argument-dependent lookup.
-// Every operation returns a normalized, weakly reduced value (< 1.03 p), so each formula's
-// inputs meet fe2_mul / fe2_sqr's bounds without bookkeeping; a product costs ~0.84 us per
-// lane instead of the engine's ~1.18 (tools/ubench/r28_bench.hip).
+// Every f_ operation returns a normalized, weakly reduced value (< 1.03 p), so each formula's
+// inputs meet fe2_mul / fe2_sqr's bounds without bookkeeping; the doubling (jac_dbl28) and the
+// Miller doubling step (line_dbl28), which dominate the chains, are written with lazy
+// combinations and their bounds instead.  A product costs ~0.84 us per lane instead of the
+// engine's ~1.18 (tools/ubench/r28_bench.hip).
 #pragma once
 #include "bls_curve.h"
 #include "bls_pairing.h"
@@ -35,7 +37,48 @@ HD void f_one(fe2 &r) {
 }
 HD bool f_is_zero(const fe2 &a) { return is_zero(a.c0) && is_zero(a.c1); }
 
+// the lazy combinations (bls_field28.h) jac_dbl28 is written in
+HD void f_add_n(fe2 &r, const fe2 &a, const fe2 &b) { fe2_add_n(r, a, b); }
+HD void f_sub_n(fe2 &r, const fe2 &a, const fe2 &b) { fe2_sub(r, a, b); }
+HD void f_mulk_n(fe2 &r, const fe2 &a, uint32_t k) { fe2_mulk_n(r, a, k); }
+template <uint32_t K>
+HD void f_subk_r(fe2 &r, const fe2 &a, const fe2 &b) {
+  fe2_subk_r<K>(r, a, b);
+}
+template <uint32_t S>
+HD void f_sub2_r(fe2 &r, const fe2 &a, const fe2 &b, const fe2 &c) {
+  fe2_sub2_r<S>(r, a, b, c);
+}
+
 typedef jac<fe2> g2j28;
+
+// dbl-2009-l as bls_curve.h jac_dbl, with lazy combinations: one normalization per combination
+// and a weak reduction only for D, X3 and Y3 (3 per coordinate field element, against 14 when
+// every addition reduces).  The jac_dbl overloads for g2j28 / g1j28 below take precedence over
+// bls_curve.h's template (argument-dependent lookup finds them from every caller, including
+// mul_by_xabs and jac_add's degenerate case).
+// Contract: input coordinates normalized and < 2.1 p; X3, Y3 < 1.03 p, Z3 normalized and
+// < 2.03 p, which every point routine of this layer accepts (jac_add's products and f_add,
+// f_neg of Y, psi, the conversions, is_zero).  r may alias p.
+template <class F>
+HD void jac_dbl28(jac<F> &r, const jac<F> &p) {
+  F A, B, C, t;
+  f_mul(t, p.y, p.z);
+  f_sqr(A, p.x);
+  f_sqr(B, p.y);
+  f_add_n(C, p.x, B);       // X + B (< 3.2 p)
+  f_add_n(r.z, t, t);       // Z3 = 2YZ (< 2.03 p)   (p.y, p.z dead)
+  f_sqr(t, C);              // (X + B)^2             (p.x dead)
+  f_sqr(C, B);              // C = B^2               (B dead)
+  f_sub2_r<2>(B, t, A, C);  // D = 2((X+B)^2 - A - C)
+  f_mulk_n(A, A, 3);        // E = 3A (< 3.1 p)
+  f_sqr(t, A);              // F = E^2
+  f_subk_r<2>(r.x, t, B);   // X3 = F - 2D
+  f_sub_n(t, B, r.x);       // D - X3 (< 5.1 p)
+  f_mul(t, A, t);           // E (D - X3)
+  f_subk_r<8>(r.y, t, C);   // Y3 = E (D - X3) - 8C
+}
+HD void jac_dbl(g2j28 &r, const g2j28 &p) { jac_dbl28(r, p); }
 
 HD void g2j_in(g2j28 &r, const g2j &a) {
   from_fp(r.x.c0, a.x.c0);
@@ -95,19 +138,13 @@ HD void fe2_half(fe2 &r, const fe2 &a) {
   half(r.c0, a.c0);
   half(r.c1, a.c1);
 }
-// 3 b' a = 12 (1 + u) a
+// 3 b' a = 12 (1 + u) a = 12 (a0 - a1) + 12 (a0 + a1) u, weakly reduced (a normalized, < 4 p)
 HD void fe2_mul_3b(fe2 &r, const fe2 &a) {
-  fe2 t, s;
-  fe2_mul_xi_r(t, a);
-  fe2_add_r(s, t, t);
-  fe2_add_r(s, s, t);
-  fe2_add_r(s, s, s);
-  fe2_add_r(r, s, s);
-}
-HD void fe2_mul3(fe2 &r, const fe2 &a) {
-  fe2 t;
-  fe2_add_r(t, a, a);
-  fe2_add_r(r, t, a);
+  fe s0, s1;
+  sub(s0, a.c0, a.c1);  // < 5.1 p
+  add_n(s1, a.c0, a.c1);
+  mulk_r(r.c0, s0, 12);
+  mulk_r(r.c1, s1, 12);
 }
 
 // ---------------------------------------------------------------- Miller line steps (k_lines)
@@ -118,37 +155,37 @@ HD void fe2_mul3(fe2 &r, const fe2 &a) {
 struct g2h28 {
   fe2 x, y, z;
 };
+// The additions are lazy (bls_field28.h "lazy point arithmetic"): each combination is
+// normalized once and weakly reduced only where a coefficient is handed out or T is updated,
+// so T keeps its bound (coordinates normalized, < 1.03 p) and every coefficient is < 1.03 p.
 template <class Put>
 HD void line_dbl28(g2h28 &T, Put &&put) {
   fe2 A, B, E, H, t;
-  fe2_sqr(B, T.y);       // Y^2
-  fe2_sqr(t, T.z);       // C = Z^2
-  fe2_mul_3b(E, t);      // 3b'Z^2
-  fe2_add_r(H, T.y, T.z);
+  fe2_sqr(B, T.y);             // Y^2
+  fe2_sqr(t, T.z);             // C = Z^2
+  fe2_mul_3b(E, t);            // 3b'Z^2
+  fe2_add_n(H, T.y, T.z);      // Y + Z (< 2.1 p)
   fe2_sqr(H, H);
-  fe2_sub_r(H, H, B);
-  fe2_sub_r(H, H, t);    // 2YZ                      (C dead)
+  fe2_sub2_r<1>(H, H, B, t);   // 2YZ                      (C dead)
   fe2_mul(A, T.x, T.y);
-  fe2_half(A, A);        // XY/2                     (Y dead)
+  fe2_half(A, A);              // XY/2                     (Y dead)
   f_neg(t, H);
-  put(4, t);             // L3 = -2YZ
+  put(4, t);                   // L3 = -2YZ
   fe2_sub_r(t, E, B);
-  put(0, t);             // L0 = 3b'Z^2 - Y^2
+  put(0, t);                   // L0 = 3b'Z^2 - Y^2
   fe2_sqr(t, T.x);
-  fe2_mul3(t, t);
-  put(2, t);             // L2 = 3X^2                (X dead)
+  fe2_mulk_r(t, t, 3);
+  put(2, t);                   // L2 = 3X^2                (X dead)
   fe2 F;
-  fe2_add_r(F, E, E);
-  fe2_add_r(F, F, E);    // 3E
-  fe2_sub_r(t, B, F);
-  fe2_mul(T.x, A, t);    // X3 = A (B - F)
-  fe2_mul(T.z, B, H);    // Z3 = B H
-  fe2_add_r(t, B, F);
-  fe2_half(t, t);
-  fe2_sqr(t, t);         // G^2
+  fe2_mulk_n(F, E, 3);         // 3E (< 3.1 p)
+  fe2_sub(t, B, F);            // B - F (< 5.1 p)
+  fe2_mul(T.x, A, t);          // X3 = A (B - F)
+  fe2_mul(T.z, B, H);          // Z3 = B H
+  fe2_add_n(t, B, F);
+  fe2_half(t, t);              // G = (B + F) / 2 (< 2.6 p)
+  fe2_sqr(t, t);               // G^2
   fe2_sqr(E, E);
-  fe2_mul3(E, E);        // 3E^2
-  fe2_sub_r(T.y, t, E);  // Y3 = G^2 - 3E^2
+  fe2_subk_r<3>(T.y, t, E);    // Y3 = G^2 - 3E^2
 }
 // T + Q for an affine Q = (qx, qy): theta = Y1 - y2 Z1, lambda = X1 - x2 Z1
 template <class Put>
@@ -236,7 +273,20 @@ HD void f_neg(fe &r, const fe &a) {
 HD void f_one(fe &r) { r = K28_ONE; }
 HD bool f_is_zero(const fe &a) { return is_zero(a); }
 
+HD void f_add_n(fe &r, const fe &a, const fe &b) { add_n(r, a, b); }
+HD void f_sub_n(fe &r, const fe &a, const fe &b) { sub(r, a, b); }
+HD void f_mulk_n(fe &r, const fe &a, uint32_t k) { mulk_n(r, a, k); }
+template <uint32_t K>
+HD void f_subk_r(fe &r, const fe &a, const fe &b) {
+  subk_r<K>(r, a, b);
+}
+template <uint32_t S>
+HD void f_sub2_r(fe &r, const fe &a, const fe &b, const fe &c) {
+  sub2_r<S>(r, a, b, c);
+}
+
 typedef jac<fe> g1j28;
+HD void jac_dbl(g1j28 &r, const g1j28 &p) { jac_dbl28(r, p); }
 
 HD void g1j28_sel(g1j28 &r, bool c, const g1j28 &a, const g1j28 &b) {  // c ? b : a
 #pragma unroll

@@ -22,6 +22,19 @@
 // for its (p-3)/4 exponentiation (unless GBLS_POW_ENGINE)
 #include <stdint.h>
 
+// Host builds with GBLS_R28_CHECK (tests/native/host_harness.cpp) abort when an operation's limb
+// contract above is broken: a product operand limb >= 2^29, a biased difference with a negative
+// limb, a value >= 2^392 where a reduction expects less.  Device code never checks.
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(GBLS_R28_CHECK)
+#include <stdlib.h>
+#define R28_CHECK(c) \
+  do {               \
+    if (!(c)) abort(); \
+  } while (0)
+#else
+#define R28_CHECK(c) ((void)0)
+#endif
+
 namespace gbls {
 namespace r28 {
 
@@ -61,6 +74,8 @@ HD void mul_n(fe &r, const fe *const *x, const fe *const *y) {
   constexpr uint32_t P[14] = {GBLS_R28_P};
   uint32_t m[14], t[14];
   uint64_t acc = 0;
+  for (int q = 0; q < NP; q++)
+    for (int i = 0; i < 14; i++) R28_CHECK(x[q]->l[i] < (1u << 29) && y[q]->l[i] < (1u << 29));
 #pragma unroll
   for (int k = 0; k < 27; k++) {
 #pragma unroll
@@ -161,9 +176,11 @@ HD void add(fe &r, const fe &a, const fe &b) {
 // 4p + a - b, normalized (b < 4p, normalized)
 HD void sub(fe &r, const fe &a, const fe &b) {
   constexpr uint32_t B[14] = {GBLS_R28_BIAS4P};
+  for (int i = 0; i < 13; i++) R28_CHECK(b.l[i] <= B[i]);
 #pragma unroll
   for (int i = 0; i < 14; i++) r.l[i] = B[i] + a.l[i] - b.l[i];
   norm(r);
+  R28_CHECK(r.l[13] < (1u << 28));
 }
 // 4p - a (a < 2p, normalized): limbs < 2^29, a product operand without normalization
 HD void neg_lazy(fe &r, const fe &a) {
@@ -245,6 +262,7 @@ HD void to_fp(fp &r, const fe &a) {
 // a - q p for q = floor(top limb / (p_top + 1)) <= a / p: a normalized (< 2^392) -> < 1.03 p
 HD void wred(fe &a) {
   constexpr uint32_t P[14] = {GBLS_R28_P};
+  for (int i = 0; i < 14; i++) R28_CHECK(a.l[i] < (1u << 28));
   const uint32_t q = a.l[13] / 0x1a012u;
   int64_t c = 0;
 #pragma unroll
@@ -257,9 +275,81 @@ HD void wred(fe &a) {
 // 8p + a - b, normalized and weakly reduced (< 1.03 p): b normalized, < 8p + a
 HD void sub_r(fe &r, const fe &a, const fe &b) {
   constexpr uint32_t B[14] = {GBLS_R28_BIAS8P};
+  for (int i = 0; i < 13; i++) R28_CHECK(b.l[i] <= B[i]);
 #pragma unroll
   for (int i = 0; i < 14; i++) r.l[i] = B[i] + a.l[i] - b.l[i];
   norm(r);
+  wred(r);
+}
+
+// ---------------------------------------------- lazy point arithmetic (bls_curve28.h)
+// The doubling formulas add and subtract up to three terms before a product or an output:
+// instead of reducing after each step (sub_r / add + wred: norm + wred, ~115 VALU per Fp), a
+// combination is formed limbwise against a bias, normalized once and weakly reduced only when
+// its consumer needs it.
+struct bias_t {
+  uint32_t l[14];
+};
+// m p with every limb but the top raised by b (2^28 - 1) (borrowed from the limb above): a
+// subtrahend with limbs <= b (2^28 - 1) leaves every limb nonnegative.  make_bias(4, 1) and
+// make_bias(8, 1) are GBLS_R28_BIAS4P / BIAS8P (static_assert below).
+constexpr bias_t make_bias(uint32_t m, uint32_t b) {
+  const uint32_t P[14] = {GBLS_R28_P};
+  bias_t r{};
+  uint64_t c = 0;
+  for (int i = 0; i < 14; i++) {
+    c += (uint64_t)m * P[i];
+    r.l[i] = (uint32_t)(c & kMask);
+    c >>= 28;
+  }
+  for (int i = 0; i < 13; i++) {
+    r.l[i] += b << 28;
+    r.l[i + 1] -= b;
+  }
+  return r;
+}
+constexpr bool bias_is(const bias_t &a, const bias_t &b) {
+  for (int i = 0; i < 14; i++)
+    if (a.l[i] != b.l[i]) return false;
+  return true;
+}
+static_assert(bias_is(make_bias(4, 1), bias_t{{GBLS_R28_BIAS4P}}), "bias generator");
+static_assert(bias_is(make_bias(8, 1), bias_t{{GBLS_R28_BIAS8P}}), "bias generator");
+
+// a + b, normalized, not reduced (a, b normalized)
+HD void add_n(fe &r, const fe &a, const fe &b) { add(r, a, b); }
+// k a, normalized, not reduced (a normalized, k <= 15)
+HD void mulk_n(fe &r, const fe &a, uint32_t k) {
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = k * a.l[i];
+  norm(r);
+}
+// k a weakly reduced (< 1.03 p): a normalized, k a < 2^392
+HD void mulk_r(fe &r, const fe &a, uint32_t k) {
+  mulk_n(r, a, k);
+  wred(r);
+}
+// a - K b weakly reduced: 16 p + a - K b with the bias raised for K normalized subtrahends;
+// a, b normalized, K b < 16 p + a, K <= 12
+template <uint32_t K>
+HD void subk_r(fe &r, const fe &a, const fe &b) {
+  constexpr bias_t B = make_bias(16, K);
+  for (int i = 0; i < 13; i++) R28_CHECK(K * b.l[i] <= B.l[i]);
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = B.l[i] + a.l[i] - K * b.l[i];
+  norm(r);
+  R28_CHECK(r.l[13] < (1u << 28));
+  wred(r);
+}
+// a - b - c weakly reduced; s = 2: 2 (a - b - c) (b, c normalized, b + c < 16 p + a)
+template <uint32_t S>
+HD void sub2_r(fe &r, const fe &a, const fe &b, const fe &c) {
+  constexpr bias_t B = make_bias(16, 2);
+  for (int i = 0; i < 13; i++) R28_CHECK(b.l[i] + c.l[i] <= B.l[i]);
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = S * (B.l[i] + a.l[i] - b.l[i] - c.l[i]);
+  norm(r);
+  R28_CHECK(r.l[13] < (1u << 28));
   wred(r);
 }
 
@@ -268,6 +358,8 @@ HD void sub_r(fe &r, const fe &a, const fe &b) {
 // output < 1.03 p
 HD void fe2_mul(fe2 &r, const fe2 &a, const fe2 &b) {
   constexpr uint32_t B[14] = {GBLS_R28_BIAS8P};
+  for (int i = 0; i < 13; i++) R28_CHECK(b.c1.l[i] <= B[i]);
+  R28_CHECK(b.c1.l[13] <= B[13]);
   fe nb1, c0;
 #pragma unroll
   for (int i = 0; i < 14; i++) nb1.l[i] = B[i] - b.c1.l[i];
@@ -277,6 +369,7 @@ HD void fe2_mul(fe2 &r, const fe2 &a, const fe2 &b) {
 }
 // (a0 + a1)(a0 - a1), 2 a0 a1
 HD void fe2_sqr(fe2 &r, const fe2 &a) {
+  for (int i = 0; i < 14; i++) R28_CHECK(a.c0.l[i] < (1u << 28) && a.c1.l[i] < (1u << 28));
   fe s, d, t;
   add_lazy(s, a.c0, a.c1);
   sub(d, a.c0, a.c1);
@@ -333,6 +426,29 @@ HD void fe2_add_r(fe2 &r, const fe2 &a, const fe2 &b) {
   add(r.c1, a.c1, b.c1);
   wred(r.c0);
   wred(r.c1);
+}
+// the lazy combinations (bls_curve28.h), per coordinate
+HD void fe2_add_n(fe2 &r, const fe2 &a, const fe2 &b) {
+  add_n(r.c0, a.c0, b.c0);
+  add_n(r.c1, a.c1, b.c1);
+}
+HD void fe2_mulk_n(fe2 &r, const fe2 &a, uint32_t k) {
+  mulk_n(r.c0, a.c0, k);
+  mulk_n(r.c1, a.c1, k);
+}
+HD void fe2_mulk_r(fe2 &r, const fe2 &a, uint32_t k) {
+  mulk_r(r.c0, a.c0, k);
+  mulk_r(r.c1, a.c1, k);
+}
+template <uint32_t K>
+HD void fe2_subk_r(fe2 &r, const fe2 &a, const fe2 &b) {
+  subk_r<K>(r.c0, a.c0, b.c0);
+  subk_r<K>(r.c1, a.c1, b.c1);
+}
+template <uint32_t S>
+HD void fe2_sub2_r(fe2 &r, const fe2 &a, const fe2 &b, const fe2 &c) {
+  sub2_r<S>(r.c0, a.c0, b.c0, c.c0);
+  sub2_r<S>(r.c1, a.c1, b.c1, c.c1);
 }
 HD void fe2_zero(fe2 &r) {
 #pragma unroll

@@ -572,3 +572,67 @@ int h_r28_g1mul_check(uint64_t seed, int n) {
 }
 
 }  // extern "C"
+
+// The lazy doubling (bls_curve28.h jac_dbl28) against bls_curve.h's jac_dbl template over the
+// reduced f_ operations, from inputs at the top of its contract (coordinates raised by p:
+// normalized, < 2.03 p; X and Y raised again every few steps), through n chained doublings of
+// r28::fe2 and r28::fe points (the formula is algebraic: no curve point needed); with
+// GBLS_R28_CHECK every combination's limb contract is checked too.  0 = all equal
+static uint32_t h_rng32(uint64_t &s) {
+  s = s * 6364136223846793005ull + 1442695040888963407ull;
+  return (uint32_t)(s >> 32);
+}
+static void h_rand(r28::fe &r, uint64_t &s) {
+  fp x;
+  for (int i = 0; i < 12; i++) x.l[i] = h_rng32(s);
+  x.l[11] &= 0x0fffffffu;  // < 2^380 < p
+  r28::from_fp(r, x);
+}
+static void h_rand(r28::fe2 &r, uint64_t &s) {
+  h_rand(r.c0, s);
+  h_rand(r.c1, s);
+}
+static void h_raise(r28::fe &a) {
+  constexpr r28::fe P = {{GBLS_R28_P}};
+  r28::add_n(a, a, P);
+}
+static void h_raise(r28::fe2 &a) {
+  h_raise(a.c0);
+  h_raise(a.c1);
+}
+static bool h_same(const r28::fe &a, const r28::fe &b) {
+  fp x, y;
+  r28::to_fp(x, a);
+  r28::to_fp(y, b);
+  return fp_eq(x, y);
+}
+static bool h_same(const r28::fe2 &a, const r28::fe2 &b) { return h_same(a.c0, b.c0) && h_same(a.c1, b.c1); }
+template <class F>
+static int h_dbl_chain(uint64_t seed, int n) {
+  uint64_t s = seed;
+  jac<F> a, b;
+  h_rand(a.x, s);
+  h_rand(a.y, s);
+  h_rand(a.z, s);
+  b = a;
+  h_raise(a.x);
+  h_raise(a.y);
+  h_raise(a.z);
+  int bad = 0;
+  for (int i = 0; i < n; i++) {
+    r28::jac_dbl28(a, a);
+    gbls::jac_dbl<F>(b, b);
+    bad += !(h_same(a.x, b.x) && h_same(a.y, b.y) && h_same(a.z, b.z));
+    if (i % 5 == 2) {
+      h_raise(a.x);
+      h_raise(a.y);
+    }
+  }
+  return bad;
+}
+extern "C" {
+int h_r28_dbl_check(uint64_t seed, int n) {
+  return h_dbl_chain<r28::fe2>(seed, n) + h_dbl_chain<r28::fe>(seed ^ 0x5bd1e995u, n);
+}
+
+}  // extern "C"

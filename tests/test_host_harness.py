@@ -34,8 +34,9 @@ def H():
     defs = os.environ.get("GBLS_HARNESS_DEFS", "").split()
     opt = (["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
            if SAN else ["-O2"])
+    # GBLS_R28_CHECK: the radix-2^28 layer's limb contracts checked on every operation (abort)
     subprocess.check_call(["g++"] + opt + ["-std=c++17", "-shared", "-fPIC", "-D__HIP_PLATFORM_AMD__",
-                           "-I/opt/rocm/include"] + defs + ["-o", SO, src])
+                           "-DGBLS_R28_CHECK", "-I/opt/rocm/include"] + defs + ["-o", SO, src])
     L = ctypes.CDLL(SO)
     L.h_multi_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
@@ -284,3 +285,13 @@ def test_radix28_g1_scalar_multiplication(H):
     for seed in (1, 77, 0xDEADBEEF):
         assert H.h_r28_g1mul_check(seed, 6) == 0, seed
 
+
+
+def test_radix28_lazy_doubling(H):
+    """bls_curve28.h jac_dbl28 (lazy combinations, weak reductions only for D, X3, Y3) equals
+    bls_curve.h's jac_dbl over the reduced f_ operations, for G2 (r28::fe2) and G1 (r28::fe)
+    coordinates, from inputs at the top of its contract (< 2.03 p) through 70 chained doublings;
+    the harness is built with GBLS_R28_CHECK, so every combination's limb contract is checked."""
+    H.h_r28_dbl_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    for seed in (1, 2, 3, 0xdeadbeef):
+        assert H.h_r28_dbl_check(seed, 70) == 0, seed
