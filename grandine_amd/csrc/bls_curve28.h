@@ -49,6 +49,14 @@ template <uint32_t S>
 HD void f_sub2_r(fe2 &r, const fe2 &a, const fe2 &b, const fe2 &c) {
   fe2_sub2_r<S>(r, a, b, c);
 }
+template <uint32_t S, uint32_t K>
+HD void f_lin_r(fe2 &r, const fe2 &a, const fe2 &b) {
+  fe2_lin_r<S, K>(r, a, b);
+}
+template <uint32_t S, uint32_t K1, uint32_t K2>
+HD void f_lin_r(fe2 &r, const fe2 &a, const fe2 &b, const fe2 &c) {
+  fe2_lin_r<S, K1, K2>(r, a, b, c);
+}
 
 typedef jac<fe2> g2j28;
 
@@ -79,6 +87,105 @@ HD void jac_dbl28(jac<F> &r, const jac<F> &p) {
   f_subk_r<8>(r.y, t, C);   // Y3 = E (D - X3) - 8C
 }
 HD void jac_dbl(g2j28 &r, const g2j28 &p) { jac_dbl28(r, p); }
+
+// add-2007-bl as bls_curve.h jac_add, with lazy combinations (3 weak reductions per field
+// element fewer).  Contract as jac_dbl28: inputs normalized, < 2.1 p; outputs < 1.03 p.
+// r may alias a (NOT b).
+template <class F>
+HD void jac_add28(jac<F> &r, const jac<F> &a, const jac<F> &b) {
+  if (jac_is_inf(b)) {
+    r = a;
+    return;
+  }
+  if (jac_is_inf(a)) {
+    r = b;
+    return;
+  }
+  F z1z1, z2z2, u1, u2, s1, s2, t;
+  f_sqr(z1z1, a.z);
+  f_sqr(z2z2, b.z);
+  f_mul(u1, a.x, z2z2);
+  f_mul(u2, b.x, z1z1);
+  f_mul(s1, a.y, b.z);
+  f_mul(s1, s1, z2z2);
+  f_mul(s2, b.y, a.z);
+  f_mul(s2, s2, z1z1);
+  f_add(t, a.z, b.z);
+  f_sqr(t, t);
+  f_sub2_r<1>(t, t, z1z1, z2z2);  // 2 Z1 Z2             (z1z1, z2z2, a.* dead)
+  f_sub(u2, u2, u1);              // H
+  f_lin_r<2, 1>(s2, s2, s1);      // r = 2 (S2 - S1)
+  if (f_is_zero(u2)) {
+    if (f_is_zero(s2))
+      jac_dbl(r, b);
+    else
+      jac_set_inf(r);
+    return;
+  }
+  f_mul(r.z, t, u2);              // Z3 = 2 Z1 Z2 H
+  f_add_n(t, u2, u2);
+  f_sqr(t, t);                    // I = (2H)^2
+  f_mul(u2, u2, t);               // J = H I
+  f_mul(u1, u1, t);               // V = U1 I
+  f_sqr(t, s2);
+  f_lin_r<1, 1, 2>(r.x, t, u2, u1);  // X3 = r^2 - J - 2V
+  f_sub_n(t, u1, r.x);            // V - X3 (< 5.1 p)
+  f_mul(t, s2, t);
+  f_mul(s1, s1, u2);
+  f_lin_r<1, 2>(r.y, t, s1);      // Y3 = r (V - X3) - 2 S1 J
+}
+
+// madd-2007-bl as bls_curve.h jac_add_aff, lazy; CHECK_B = false when b is known finite (the
+// MSM's bucket points: no zero test of b).  r may alias a.
+template <bool CHECK_B, class F>
+HD void jac_add_aff28(jac<F> &r, const jac<F> &a, const aff<F> &b) {
+  if (CHECK_B && aff_is_inf(b)) {
+    r = a;
+    return;
+  }
+  if (jac_is_inf(a)) {
+    r.x = b.x;
+    r.y = b.y;
+    f_one(r.z);
+    if (CHECK_B && aff_is_inf(b)) f_zero(r.z);
+    return;
+  }
+  F z1z1, u2, s2, t, hh;
+  f_sqr(z1z1, a.z);
+  f_mul(u2, b.x, z1z1);
+  f_mul(s2, b.y, a.z);
+  f_mul(s2, s2, z1z1);
+  f_sub(u2, u2, a.x);             // H
+  f_lin_r<2, 1>(s2, s2, a.y);     // r = 2 (S2 - Y1)
+  if (f_is_zero(u2)) {
+    if (f_is_zero(s2)) {
+      jac<F> bj;
+      bj.x = b.x;
+      bj.y = b.y;
+      f_one(bj.z);
+      jac_dbl(r, bj);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  f_add_n(t, a.z, u2);            // Z1 + H (< 3.2 p)
+  f_sqr(t, t);
+  f_sqr(hh, u2);
+  f_sub2_r<1>(r.z, t, z1z1, hh);  // Z3 = (Z1 + H)^2 - Z1Z1 - HH   (a.z dead)
+  f_mulk_n(hh, hh, 4);            // I = 4 HH (< 4.1 p)
+  f_mul(z1z1, a.x, hh);           // V = X1 I
+  f_mul(hh, u2, hh);              // J = H I
+  f_mul(t, a.y, hh);              // Y1 J                    (a.x, a.y dead)
+  f_sqr(u2, s2);
+  f_lin_r<1, 1, 2>(r.x, u2, hh, z1z1);  // X3 = r^2 - J - 2V
+  f_sub_n(u2, z1z1, r.x);         // V - X3 (< 5.1 p)
+  f_mul(u2, s2, u2);
+  f_lin_r<1, 2>(r.y, u2, t);      // Y3 = r (V - X3) - 2 Y1 J
+}
+typedef aff<fe2> g2a28;
+HD void jac_add(g2j28 &r, const g2j28 &a, const g2j28 &b) { jac_add28(r, a, b); }
+HD void jac_add_aff(g2j28 &r, const g2j28 &a, const g2a28 &b) { jac_add_aff28<true>(r, a, b); }
 
 HD void g2j_in(g2j28 &r, const g2j &a) {
   from_fp(r.x.c0, a.x.c0);
@@ -227,6 +334,26 @@ HD void line_add28(g2h28 &T, const fe2 &qx, const fe2 &qy, Put &&put) {
 // 2^392 mod p, which an engine-form reader sees as the value times 2^8)
 HD void store12(fp &dst, const fe &a) { repack_out(dst, a); }
 HD void load12(fe &r, const fp &src) { repack_in(r, src); }
+// points in engine-layout slots, coordinate by coordinate (store12 / load12): the clearing
+// chains' intermediate points and the MSM's signatures and bucket partials
+HD void g2j_store12(g2j &dst, const g2j28 &a) {
+  store12(dst.x.c0, a.x.c0), store12(dst.x.c1, a.x.c1);
+  store12(dst.y.c0, a.y.c0), store12(dst.y.c1, a.y.c1);
+  store12(dst.z.c0, a.z.c0), store12(dst.z.c1, a.z.c1);
+}
+HD void g2j_load12(g2j28 &r, const g2j &src) {
+  load12(r.x.c0, src.x.c0), load12(r.x.c1, src.x.c1);
+  load12(r.y.c0, src.y.c0), load12(r.y.c1, src.y.c1);
+  load12(r.z.c0, src.z.c0), load12(r.z.c1, src.z.c1);
+}
+HD void g2a_store12(g2a &dst, const g2a28 &a) {
+  store12(dst.x.c0, a.x.c0), store12(dst.x.c1, a.x.c1);
+  store12(dst.y.c0, a.y.c0), store12(dst.y.c1, a.y.c1);
+}
+HD void g2a_load12(g2a28 &r, const g2a &src) {
+  load12(r.x.c0, src.x.c0), load12(r.x.c1, src.x.c1);
+  load12(r.y.c0, src.y.c0), load12(r.y.c1, src.y.c1);
+}
 
 // h_eff P, the sequence of clear_cofactor_g2 (bls_hash.h, Budroni-Pintore): host tests of
 // the layer's G2 formulas (tests/native/host_harness.cpp)
@@ -284,9 +411,18 @@ template <uint32_t S>
 HD void f_sub2_r(fe &r, const fe &a, const fe &b, const fe &c) {
   sub2_r<S>(r, a, b, c);
 }
+template <uint32_t S, uint32_t K>
+HD void f_lin_r(fe &r, const fe &a, const fe &b) {
+  lin_r<S, K>(r, a, b);
+}
+template <uint32_t S, uint32_t K1, uint32_t K2>
+HD void f_lin_r(fe &r, const fe &a, const fe &b, const fe &c) {
+  lin_r<S, K1, K2>(r, a, b, c);
+}
 
 typedef jac<fe> g1j28;
 HD void jac_dbl(g1j28 &r, const g1j28 &p) { jac_dbl28(r, p); }
+HD void jac_add(g1j28 &r, const g1j28 &a, const g1j28 &b) { jac_add28(r, a, b); }
 
 HD void g1j28_sel(g1j28 &r, bool c, const g1j28 &a, const g1j28 &b) {  // c ? b : a
 #pragma unroll

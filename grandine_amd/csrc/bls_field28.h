@@ -329,28 +329,40 @@ HD void mulk_r(fe &r, const fe &a, uint32_t k) {
   mulk_n(r, a, k);
   wred(r);
 }
-// a - K b weakly reduced: 16 p + a - K b with the bias raised for K normalized subtrahends;
-// a, b normalized, K b < 16 p + a, K <= 12
-template <uint32_t K>
-HD void subk_r(fe &r, const fe &a, const fe &b) {
-  constexpr bias_t B = make_bias(16, K);
-  for (int i = 0; i < 13; i++) R28_CHECK(K * b.l[i] <= B.l[i]);
+// S (a - K1 b - K2 c) weakly reduced (< 1.03 p): formed limbwise against 16 p raised for
+// K1 + K2 normalized subtrahend limbs, normalized once; a, b, c normalized,
+// K1 b + K2 c < 16 p + a, S (K1 + K2 + 2) <= 15 (every limb < 2^32)
+template <uint32_t S, uint32_t K1, uint32_t K2>
+HD void lin_r(fe &r, const fe &a, const fe &b, const fe &c) {
+  static_assert(S * (K1 + K2 + 2) <= 15, "limb bound");
+  constexpr bias_t B = make_bias(16, K1 + K2);
+  for (int i = 0; i < 13; i++) R28_CHECK(K1 * b.l[i] + K2 * c.l[i] <= B.l[i]);
 #pragma unroll
-  for (int i = 0; i < 14; i++) r.l[i] = B.l[i] + a.l[i] - K * b.l[i];
+  for (int i = 0; i < 14; i++) r.l[i] = S * (B.l[i] + a.l[i] - K1 * b.l[i] - K2 * c.l[i]);
   norm(r);
   R28_CHECK(r.l[13] < (1u << 28));
   wred(r);
 }
-// a - b - c weakly reduced; s = 2: 2 (a - b - c) (b, c normalized, b + c < 16 p + a)
-template <uint32_t S>
-HD void sub2_r(fe &r, const fe &a, const fe &b, const fe &c) {
-  constexpr bias_t B = make_bias(16, 2);
-  for (int i = 0; i < 13; i++) R28_CHECK(b.l[i] + c.l[i] <= B.l[i]);
+// S (a - K b), the same
+template <uint32_t S, uint32_t K>
+HD void lin_r(fe &r, const fe &a, const fe &b) {
+  static_assert(S * (K + 2) <= 15, "limb bound");
+  constexpr bias_t B = make_bias(16, K);
+  for (int i = 0; i < 13; i++) R28_CHECK(K * b.l[i] <= B.l[i]);
 #pragma unroll
-  for (int i = 0; i < 14; i++) r.l[i] = S * (B.l[i] + a.l[i] - b.l[i] - c.l[i]);
+  for (int i = 0; i < 14; i++) r.l[i] = S * (B.l[i] + a.l[i] - K * b.l[i]);
   norm(r);
   R28_CHECK(r.l[13] < (1u << 28));
   wred(r);
+}
+// a - K b; S (a - b - c)
+template <uint32_t K>
+HD void subk_r(fe &r, const fe &a, const fe &b) {
+  lin_r<1, K>(r, a, b);
+}
+template <uint32_t S>
+HD void sub2_r(fe &r, const fe &a, const fe &b, const fe &c) {
+  lin_r<S, 1, 1>(r, a, b, c);
 }
 
 // ------------------------------------------------------------------ Fp2 = Fp[u] / (u^2 + 1)
@@ -449,6 +461,16 @@ template <uint32_t S>
 HD void fe2_sub2_r(fe2 &r, const fe2 &a, const fe2 &b, const fe2 &c) {
   sub2_r<S>(r.c0, a.c0, b.c0, c.c0);
   sub2_r<S>(r.c1, a.c1, b.c1, c.c1);
+}
+template <uint32_t S, uint32_t K>
+HD void fe2_lin_r(fe2 &r, const fe2 &a, const fe2 &b) {
+  lin_r<S, K>(r.c0, a.c0, b.c0);
+  lin_r<S, K>(r.c1, a.c1, b.c1);
+}
+template <uint32_t S, uint32_t K1, uint32_t K2>
+HD void fe2_lin_r(fe2 &r, const fe2 &a, const fe2 &b, const fe2 &c) {
+  lin_r<S, K1, K2>(r.c0, a.c0, b.c0, c.c0);
+  lin_r<S, K1, K2>(r.c1, a.c1, b.c1, c.c1);
 }
 HD void fe2_zero(fe2 &r) {
 #pragma unroll

@@ -49,6 +49,7 @@ static_assert(sizeof(fp12) == sizeof(gbls_fp12), "fp12 layout");
 uint32_t gbls::g_row_clear_max = gbls::kRowClearMax;
 uint32_t gbls::g_ml_r28 = 1;
 uint32_t gbls::g_msm_k = gbls::kMsmChunk;
+uint32_t gbls::g_msm_r28 = 1;
 uint32_t gbls::g_ml_xcd = 1;
 uint32_t gbls::g_ml_dma = 0;
 uint32_t gbls::g_ml_prefetch = 1;
@@ -575,6 +576,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
       g_row_clear_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_CU_SPLIT")) g.cu_split = std::atoi(e);
     if (const char *e = std::getenv("GBLS_MSM_K")) g_msm_k = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char *e = std::getenv("GBLS_MSM_R28")) g_msm_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_ML_XCD")) g_ml_xcd = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LANE_R28")) g_lane_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_CU_SPLIT_MAX"))

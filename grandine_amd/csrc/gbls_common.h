@@ -43,6 +43,7 @@ constexpr uint32_t kMsmChunk = 16;
 constexpr int kMsmFoldLevels = 3;        // k_msm_fold: pairwise levels over each bucket's partials
 constexpr uint32_t kMsmFold = 1u << kMsmFoldLevels;  // chunk partials per fold group
 extern uint32_t g_msm_k;                 // kMsmChunk unless GBLS_MSM_K is set
+extern uint32_t g_msm_r28;               // k_msm_chunk28 / k_msm_fold28 (GBLS_MSM_R28=0: the engine-form kernels)
 extern uint32_t g_ml_kara;               // k_ml_group28: Karatsuba Fp2 sparse products (GBLS_ML_KARA)
 extern uint32_t g_ml_prefetch;           // k_ml_group28: next pair's line loaded during the product (GBLS_ML_PREFETCH)
 extern uint32_t g_ml_dma;                // k_ml_group28: line staged in LDS by DMA loads (GBLS_ML_DMA)
@@ -116,7 +117,9 @@ struct MsmPlan {
   uint32_t max_folds;   // bound on the level-0 fold-pair count (grid of the fold kernels)
   bool tree;            // per-window bucket trees (c = 13) or per-bucket pairs (c = 5)
   uint32_t extra;       // extra Miller pairs per segment: W (tree) or W * 2^(c-1)
-  size_t o_cnt, o_start, o_cur, o_cstart, o_fstart[kMsmFoldLevels], o_list, o_chunk, o_t0, o_a0, o_t1, o_a1, bytes;
+  bool r28;             // chunk sums and folds in radix 2^28 (g_msm_r28)
+  size_t o_cnt, o_start, o_cur, o_cstart, o_fstart[kMsmFoldLevels], o_list, o_chunk, o_t0, o_a0, o_t1, o_a1,
+      o_sig28, bytes;
 };
 // default: segments at least this large use the bucket MSM (2048 -> 4096 in r04: a C4 epoch of
 // 2048-set segments ran 542-572k sets/s with per-set products vs 375-390k with the MSM,

@@ -151,16 +151,8 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane_b(const g2j *Q, uint32_t 
 // free of scratch; between the chains the message's Q slots hold the radix-2^28 limbs repacked
 // into the engine layout (store12, no conversion product); chain b converts its result to
 // engine form (to_fp) before the affine conversion, so H is bit-identical to the 32-bit path's.
-__device__ __forceinline__ void g2j28_store(g2j &dst, const r28::g2j28 &a) {
-  r28::store12(dst.x.c0, a.x.c0), r28::store12(dst.x.c1, a.x.c1);
-  r28::store12(dst.y.c0, a.y.c0), r28::store12(dst.y.c1, a.y.c1);
-  r28::store12(dst.z.c0, a.z.c0), r28::store12(dst.z.c1, a.z.c1);
-}
-__device__ __forceinline__ void g2j28_load(r28::g2j28 &r, const g2j &src) {
-  r28::load12(r.x.c0, src.x.c0), r28::load12(r.x.c1, src.x.c1);
-  r28::load12(r.y.c0, src.y.c0), r28::load12(r.y.c1, src.y.c1);
-  r28::load12(r.z.c0, src.z.c0), r28::load12(r.z.c1, src.z.c1);
-}
+__device__ __forceinline__ void g2j28_store(g2j &dst, const r28::g2j28 &a) { r28::g2j_store12(dst, a); }
+__device__ __forceinline__ void g2j28_load(r28::g2j28 &r, const g2j &src) { r28::g2j_load12(r, src); }
 // A chain's base point in LDS, one per lane at an ODD stride of 85 words (84 + 1 pad): the 4-byte
 // LDS accesses of the 32 lanes of a group then fall in 32 different banks (the unpadded stride
 // of 84 = 4 x 21 words put every 4th lane on one bank: 4-way conflicts, 58 % of the kernels'

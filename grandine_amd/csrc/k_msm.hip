@@ -41,8 +41,15 @@
 // signatures; a zero scalar fails the batch through k_msm_count's flags).  An empty bucket is
 // the point at infinity, whose Miller pair is the identity.  Bucket order is
 // nondeterministic (atomics) but the sums are exact, so the verdict is too.
+//
+// r06: the chunk sums and the fold levels run in radix 2^28 (k_msm_chunk28 / k_msm_fold28,
+// bls_curve28.h's lazy jac_add_aff28 / jac_add28): k_msm_count writes each scattered
+// signature once in radix 2^28 (4 conversion products per set, against ~13 additions of it),
+// partials are stored as radix-2^28 limbs in the engine layout (store12), and the bucket
+// readers (k_msm_pairs / k_msm_bucket) convert their sums back to engine form.
 #include "gbls_common.h"
 #include "bls_gang.h"
+#include "bls_curve28.h"
 
 namespace gbls {
 
@@ -77,14 +84,21 @@ __global__ void __launch_bounds__(WGR) k_msm_count(const g2a *sigs, const uint64
                                                    const uint32_t *seg_off, uint32_t nseg, int c,
                                                    int W, const g1a *pks, const int32_t *pre,
                                                    const int32_t *pre2, uint32_t *cnt,
-                                                   int32_t *seg_err) {
+                                                   int32_t *seg_err, g2a *sig28) {
   uint32_t i = blockIdx.x * WGR + threadIdx.x;
   if (i >= n) return;
   uint64_t k = rands[i];
   const uint32_t s = msm_segment(seg_off, nseg, i);
   if (aff_is_inf(pks[i]) || k == 0 || (pre && pre[i] != 0) || (pre2 && pre2[i] != 0))
     atomicOr(&seg_err[s], 1);
-  if (k == 0 || aff_is_inf(sigs[i])) return;
+  const g2a sg = sigs[i];
+  if (k == 0 || aff_is_inf(sg)) return;
+  if (sig28) {  // the signature in radix 2^28 for k_msm_chunk28 (every scattered set)
+    r28::g2a28 a;
+    r28::from_fp(a.x.c0, sg.x.c0), r28::from_fp(a.x.c1, sg.x.c1);
+    r28::from_fp(a.y.c0, sg.y.c0), r28::from_fp(a.y.c1, sg.y.c1);
+    r28::g2a_store12(sig28[i], a);
+  }
   const uint32_t B = 1u << (c - 1);
   const uint32_t base = s * (uint32_t)W * B;
   uint32_t carry = 0;
@@ -224,8 +238,57 @@ __global__ void __launch_bounds__(WG) k_msm_fold(const uint32_t *cstart, const u
   chunk[j] = x;
 }
 
+// k_msm_chunk in radix 2^28: the bucket's points from sig28 (radix-2^28 limbs, never infinite:
+// k_msm_scatter lists finite signatures only), the partial stored as radix-2^28 limbs
+__global__ void __launch_bounds__(WG) k_msm_chunk28(const g2a *sig28, const uint32_t *list,
+                                                    const uint32_t *start, const uint32_t *cstart,
+                                                    uint32_t nb, uint32_t max_chunks, uint32_t K,
+                                                    g2j *chunk) {
+  const uint32_t j = blockIdx.x * WG + threadIdx.x;
+  if (j >= max_chunks || j >= cstart[nb]) return;
+  const uint32_t b = msm_owner(cstart, nb, j);
+  const uint32_t e0 = start[b] + (j - cstart[b]) * K;
+  const uint32_t e1 = min(e0 + K, start[b + 1]);
+  r28::g2j28 acc;
+  uint32_t vn = list[e0];
+  g2a pn = sig28[vn & 0x7fffffffu];
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint32_t v = vn;
+    r28::g2a28 q;
+    r28::g2a_load12(q, pn);
+    if (e + 1 < e1) {
+      vn = list[e + 1];
+      pn = sig28[vn & 0x7fffffffu];
+    }
+    if (v >> 31) r28::f_neg(q.y, q.y);
+    if (e == e0) {
+      acc.x = q.x;
+      acc.y = q.y;
+      r28::f_one(acc.z);
+    } else {
+      r28::jac_add_aff28<false>(acc, acc, q);
+    }
+  }
+  r28::g2j_store12(chunk[j], acc);
+}
+__global__ void __launch_bounds__(WG) k_msm_fold28(const uint32_t *cstart, const uint32_t *fstart,
+                                                   uint32_t nb, uint32_t max_pairs, int l,
+                                                   g2j *chunk) {
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= max_pairs || t >= fstart[nb]) return;
+  const uint32_t b = msm_owner(fstart, nb, t);
+  const uint32_t j = cstart[b] + ((t - fstart[b]) << (l + 1));
+  r28::g2j28 x, y;
+  r28::g2j_load12(x, chunk[j]);
+  r28::g2j_load12(y, chunk[j + (1u << l)]);
+  jac_add(x, x, y);
+  r28::g2j_store12(chunk[j], x);
+}
+
 // sum of bucket b: its fold groups' sums (k_msm_fold), at every kMsmFold-th chunk partial of
 // the bucket's chunk range
+// (R28: the partials are radix-2^28 limbs, summed in radix 2^28 and converted to engine form)
+template <bool R28>
 __device__ __forceinline__ void msm_bucket_sum(g2j &x, const g2j *chunk, const uint32_t *cstart,
                                                uint32_t b) {
   const uint32_t c0 = cstart[b], c1 = cstart[b + 1];
@@ -233,10 +296,20 @@ __device__ __forceinline__ void msm_bucket_sum(g2j &x, const g2j *chunk, const u
     jac_set_inf(x);
     return;
   }
-  x = chunk[c0];
-  for (uint32_t w = c0 + kMsmFold; w < c1; w += kMsmFold) {
-    g2j y = chunk[w];
-    jac_add(x, x, y);
+  if constexpr (R28) {
+    r28::g2j28 s, y;
+    r28::g2j_load12(s, chunk[c0]);
+    for (uint32_t w = c0 + kMsmFold; w < c1; w += kMsmFold) {
+      r28::g2j_load12(y, chunk[w]);
+      jac_add(s, s, y);
+    }
+    r28::g2j_out(x, s);
+  } else {
+    x = chunk[c0];
+    for (uint32_t w = c0 + kMsmFold; w < c1; w += kMsmFold) {
+      g2j y = chunk[w];
+      jac_add(x, x, y);
+    }
   }
 }
 
@@ -252,6 +325,7 @@ __device__ __forceinline__ void msm_weight(g1s &o, const uint32_t *table, uint32
 
 // c = 5: lane per bucket t = s * W * B + k; its sum X (the bucket's folded first chunk, or
 // infinity) pairs with -[(b+1) 2^(c w)] g1 at pair n + t
+template <bool R28>
 __global__ void __launch_bounds__(WG) k_msm_pairs(const g2j *chunk, const uint32_t *cstart,
                                                   uint32_t nb, uint32_t per_seg, uint32_t n,
                                                   const uint32_t *seg_off, int empty_is_error,
@@ -260,7 +334,7 @@ __global__ void __launch_bounds__(WG) k_msm_pairs(const g2j *chunk, const uint32
   if (t >= nb) return;
   uint32_t s = t / per_seg, k = t % per_seg;
   g2j x;
-  msm_bucket_sum(x, chunk, cstart, t);
+  msm_bucket_sum<R28>(x, chunk, cstart, t);
   g2a a;
   jac_to_aff(a, x);
   g1s w;
@@ -271,12 +345,13 @@ __global__ void __launch_bounds__(WG) k_msm_pairs(const g2j *chunk, const uint32
 }
 
 // level-0 tree nodes: T = X_b (the bucket's folded first chunk, or infinity), A = inf
+template <bool R28>
 __global__ void __launch_bounds__(WG) k_msm_bucket(const g2j *chunk, const uint32_t *cstart,
                                                    uint32_t nb, g2j *T, g2j *A) {
   uint32_t b = blockIdx.x * WG + threadIdx.x;
   if (b >= nb) return;
   g2j x, inf;
-  msm_bucket_sum(x, chunk, cstart, b);
+  msm_bucket_sum<R28>(x, chunk, cstart, b);
   jac_set_inf(inf);
   T[b] = x;
   A[b] = inf;
@@ -357,6 +432,8 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.o_a0 = take(tn * sizeof(g2j));
   p.o_t1 = take((tn / 2 + 1) * sizeof(g2j));
   p.o_a1 = take((tn / 2 + 1) * sizeof(g2j));
+  p.r28 = g_msm_r28 != 0;
+  p.o_sig28 = take(p.r28 ? (size_t)n * sizeof(g2a) : 0);
   p.bytes = o;
   return p;
 }
@@ -375,25 +452,40 @@ void launch_msm(hipStream_t st, const MsmPlan &p, uint8_t *ws, const g2a *sigs,
   g2j *chunk = reinterpret_cast<g2j *>(ws + p.o_chunk);
   (void)hipMemsetAsync(cnt, 0, p.nb * 4, st);
   (void)hipMemsetAsync(seg_err, 0, p.nseg * 4, st);
+  g2a *sig28 = p.r28 ? reinterpret_cast<g2a *>(ws + p.o_sig28) : nullptr;
   k_msm_count<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, pks, pre,
-                                            pre2, cnt, seg_err);
+                                            pre2, cnt, seg_err, sig28);
   k_msm_scan<<<1, 1024, 0, st>>>(cnt, p.nb, p.K, start, cur, cstart, fs);
   k_msm_scatter<<<nblk(n, WGR), WGR, 0, st>>>(sigs, rands, n, seg_off, p.nseg, p.c, p.W, cur,
                                               list);
-  k_msm_chunk<<<nblk(p.max_chunks), WG, 0, st>>>(sigs, list, start, cstart, p.nb, p.max_chunks,
-                                                 p.K, chunk);
+  if (p.r28)
+    k_msm_chunk28<<<nblk(p.max_chunks), WG, 0, st>>>(sig28, list, start, cstart, p.nb, p.max_chunks,
+                                                     p.K, chunk);
+  else
+    k_msm_chunk<<<nblk(p.max_chunks), WG, 0, st>>>(sigs, list, start, cstart, p.nb, p.max_chunks,
+                                                   p.K, chunk);
   for (int l = 0; l < kMsmFoldLevels; l++) {
     const uint32_t mp = (p.max_folds >> l) + p.nb;
-    k_msm_fold<<<nblk(mp), WG, 0, st>>>(cstart, fs.l[l], p.nb, mp, l, chunk);
+    if (p.r28)
+      k_msm_fold28<<<nblk(mp), WG, 0, st>>>(cstart, fs.l[l], p.nb, mp, l, chunk);
+    else
+      k_msm_fold<<<nblk(mp), WG, 0, st>>>(cstart, fs.l[l], p.nb, mp, l, chunk);
   }
   if (!p.tree) {
-    k_msm_pairs<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, p.extra, n, seg_off,
-                                           empty_is_error, P, H, seg_err);
+    if (p.r28)
+      k_msm_pairs<true><<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, p.extra, n, seg_off,
+                                                   empty_is_error, P, H, seg_err);
+    else
+      k_msm_pairs<false><<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, p.extra, n, seg_off,
+                                                    empty_is_error, P, H, seg_err);
     return;
   }
   g2j *T[2] = {reinterpret_cast<g2j *>(ws + p.o_t0), reinterpret_cast<g2j *>(ws + p.o_t1)};
   g2j *A[2] = {reinterpret_cast<g2j *>(ws + p.o_a0), reinterpret_cast<g2j *>(ws + p.o_a1)};
-  k_msm_bucket<<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, T[0], A[0]);
+  if (p.r28)
+    k_msm_bucket<true><<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, T[0], A[0]);
+  else
+    k_msm_bucket<false><<<nblk(p.nb), WG, 0, st>>>(chunk, cstart, p.nb, T[0], A[0]);
   int src = 0;
   const uint32_t B = 1u << (p.c - 1), groups = p.nseg * (uint32_t)p.W;
   for (int l = 0; (1u << (l + 1)) <= B; l++) {

@@ -573,8 +573,8 @@ int h_r28_g1mul_check(uint64_t seed, int n) {
 
 }  // extern "C"
 
-// The lazy doubling (bls_curve28.h jac_dbl28) against bls_curve.h's jac_dbl template over the
-// reduced f_ operations, from inputs at the top of its contract (coordinates raised by p:
+// The lazy doubling and additions (bls_curve28.h jac_dbl28 / jac_add28 / jac_add_aff28) against
+// bls_curve.h's templates over the reduced f_ operations, from inputs at the top of its contract (coordinates raised by p:
 // normalized, < 2.03 p; X and Y raised again every few steps), through n chained doublings of
 // r28::fe2 and r28::fe points (the formula is algebraic: no curve point needed); with
 // GBLS_R28_CHECK every combination's limb contract is checked too.  0 = all equal
@@ -623,6 +623,26 @@ static int h_dbl_chain(uint64_t seed, int n) {
     r28::jac_dbl28(a, a);
     gbls::jac_dbl<F>(b, b);
     bad += !(h_same(a.x, b.x) && h_same(a.y, b.y) && h_same(a.z, b.z));
+    if (i % 3 == 1) {  // + a Jacobian point (its lazy copy raised to < 2.03 p)
+      jac<F> c, cr;
+      h_rand(c.x, s);
+      h_rand(c.y, s);
+      h_rand(c.z, s);
+      cr = c;
+      h_raise(cr.x);
+      h_raise(cr.z);
+      r28::jac_add28(a, a, cr);
+      gbls::jac_add<F>(b, b, c);
+      bad += !(h_same(a.x, b.x) && h_same(a.y, b.y) && h_same(a.z, b.z));
+    }
+    if (i % 3 == 2) {  // + an affine point
+      aff<F> q;
+      h_rand(q.x, s);
+      h_rand(q.y, s);
+      r28::jac_add_aff28<true>(a, a, q);
+      gbls::jac_add_aff<F>(b, b, q);
+      bad += !(h_same(a.x, b.x) && h_same(a.y, b.y) && h_same(a.z, b.z));
+    }
     if (i % 5 == 2) {
       h_raise(a.x);
       h_raise(a.y);

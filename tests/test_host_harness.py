@@ -288,9 +288,11 @@ def test_radix28_g1_scalar_multiplication(H):
 
 
 def test_radix28_lazy_doubling(H):
-    """bls_curve28.h jac_dbl28 (lazy combinations, weak reductions only for D, X3, Y3) equals
-    bls_curve.h's jac_dbl over the reduced f_ operations, for G2 (r28::fe2) and G1 (r28::fe)
-    coordinates, from inputs at the top of its contract (< 2.03 p) through 70 chained doublings;
+    """bls_curve28.h jac_dbl28 / jac_add28 / jac_add_aff28 (lazy combinations, weak reductions
+    only where an output or a square's operand needs one) equal bls_curve.h's jac_dbl / jac_add /
+    jac_add_aff over the reduced f_ operations, for G2 (r28::fe2) and G1 (r28::fe) coordinates,
+    from inputs at the top of their contract (< 2.03 p) through 70 chained doublings with an
+    addition of a Jacobian or an affine point after two of every three;
     the harness is built with GBLS_R28_CHECK, so every combination's limb contract is checked."""
     H.h_r28_dbl_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
     for seed in (1, 2, 3, 0xdeadbeef):
