@@ -365,7 +365,9 @@ def main():
         d_msgs, d_sigs = dbytes(msgs), dbytes(bytes(sigs))
         d_idx = dnp(np.tile(committee, m))
         d_off = dnp(np.arange(0, k * m + 1, k, dtype=np.uint32))
-        d_v = torch.full((m,), -1, dtype=torch.int32, device=dev)
+        # one verdict buffer per in-flight slot (two submissions at once, as C2)
+        d_vs = [torch.full((m,), -1, dtype=torch.int32, device=dev) for _ in range(max(1, args.inflight))]
+        torch.cuda.synchronize()
         want = torch.zeros(m, dtype=torch.int32)
         want[invalid] = G.VERIFY_FAIL
         leg.units = m
@@ -376,10 +378,10 @@ def main():
 
         def step(slot=0):
             G.check(L.gbls_fast_aggregate_verify_indexed_device(ptr(d_sigs), ptr(d_msgs), ptr(d_idx), ptr(d_off), m,
-                                                                ptr(d_v), cur_stream()), "fav indexed device")
+                                                                ptr(d_vs[slot]), cur_stream()), "fav indexed device")
 
         def verdict_ok():
-            return bool(torch.equal(d_v.cpu(), want))
+            return all(bool(torch.equal(v.cpu(), want)) for v in d_vs)
 
         # Batches of 2048..65536 checks take the grouped form (gbls_capi.hip grouped_verdicts):
         # r_i-weighted pairs, one Horner step + final exponentiation per group of GROUP checks,
@@ -405,7 +407,7 @@ def main():
     else:
         return bench_c1(args, L, G, F, np)
 
-    D = max(1, args.inflight) if cfg != "C3" else 1
+    D = max(1, args.inflight)
     streams = [torch.cuda.Stream() for _ in range(D)] if D > 1 else None
 
     def run(k):
