@@ -99,9 +99,11 @@ def pmc_traffic(kernel, default_cmd):
     summary of the default command's 16-batch launches (profiles/r06/z_c2_pmc_bytes.csv,
     tools/prof/pmc_bytes.py --largest; FETCH_SIZE doubled per the gfx950 correction).  None for
     other commands or if absent."""
-    path = os.path.join(ROOT, "profiles", "r06", "z_c2_pmc_bytes.csv")
-    if not os.path.exists(path):  # the round's checkpoint pass until the final one is committed
-        path = os.path.join(ROOT, "profiles", "r06", "o_c2_pmc_bytes.csv")
+    # the round's final pass, else its latest checkpoint pass
+    for tag in ("z", "x", "o"):
+        path = os.path.join(ROOT, "profiles", "r06", tag + "_c2_pmc_bytes.csv")
+        if os.path.exists(path):
+            break
     if not default_cmd or not os.path.exists(path):
         return None
     with open(path) as f:

@@ -276,7 +276,7 @@ void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   if (!n) return;
   if (n <= kW4Max)
     (n <= w4::kExclusiveMaxWaves ? k_h2c_clear_w4<true> : k_h2c_clear_w4<false>)<<<n, 64, 0, st>>>(Q, n, H);
-  else if (n >= kLaneRegimeClear) {
+  else if (n >= g_lane_min) {
     // Q is a scratch of the call (the map's output); its two slots per message carry the
     // points between the two chains
     if (g_lane_r28) {

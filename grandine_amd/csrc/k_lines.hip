@@ -403,9 +403,9 @@ void launch_lines(hipStream_t st, const g2a *H, uint32_t first, uint32_t count, 
   if (count <= kW4Max)
     (count <= w4::kExclusiveMaxWaves ? k_lines_w4<true> : k_lines_w4<false>)<<<count, 64, 0, st>>>(
         H, first, count, lc, e0, e1, Ts, lines);
-  else if (count >= kLaneRegimeLines && g_lane_r28)
+  else if (count >= g_lane_min && g_lane_r28)
     k_lines_lane28<<<nblk(count), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);
-  else if (count >= kLaneRegimeLines)
+  else if (count >= g_lane_min)
     k_lines_lane<<<nblk(count), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);
   else if (count <= kRowRegimeMax)
     k_lines_row<<<nblk((size_t)count * 16), WG, 0, st>>>(H, first, count, lc, e0, e1, Ts, lines);

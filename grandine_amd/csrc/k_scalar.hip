@@ -294,9 +294,9 @@ void launch_mv_g1mul(hipStream_t st, const g1a *pks, const uint64_t *rands, uint
     launch_mv_g1mul_w4(st, pks, rands, n, P);
     return;
   }
-  if (n >= kLaneRegimeSets && g_lane_r28)
+  if (n >= g_lane_min && g_lane_r28)
     k_mv_g1mul_lane28<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
-  else if (n >= kLaneRegimeSets)
+  else if (n >= g_lane_min)
     k_mv_g1mul_lane<<<nblk(n), WG, 0, st>>>(pks, rands, n, P);
   else
     (nblk(4 * (size_t)n) <= w4::kExclusiveMaxWaves ? k_mv_g1mul<true> : k_mv_g1mul<false>)<<<

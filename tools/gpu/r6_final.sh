@@ -27,7 +27,7 @@ for f in $O/bench_*.txt; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f
 step trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- $B > $O/trace.log 2>&1 || exit $?
 python3 tools/prof/db_stats.py $(ls $O/trace/*.db | head -1) > $O/c2_kernel_stats.csv &&
-python3 tools/prof/join_wait.py $(ls $O/trace/*.db | head -1) 100000 > $O/c2_join_wait.txt &&
+python3 tools/prof/join_wait.py $(ls $O/trace/*.db | head -1) 60000 > $O/c2_join_wait.txt &&
 python3 tools/prof/timeline.py $(ls $O/trace/*.db | head -1) 3 k_mv_g1mul > $O/c2_timeline.txt || exit $?
 tail -1 $O/c2_join_wait.txt
 step pmc
