@@ -16,10 +16,12 @@ constexpr uint32_t NONE = 0xffffffffu;
 // Stages with a quad-gang (latency) and a lane-per-item (throughput) variant pick the
 // latter from these launch sizes on (measured on MI355X, 12 x 4096-set C2 step: Miller lines
 // 3.32 ms quad vs 2.44 ms lane at 49152 pairs; cofactor clearing 4.99 vs 4.40 ms at 32768
-// sets, the other streams filling the SIMDs a lane launch leaves free).
-constexpr uint32_t kLaneRegimeSets = 32768;   // G1 products, MSM folds
-constexpr uint32_t kLaneRegimeClear = 32768;  // cofactor clearing
-constexpr uint32_t kLaneRegimeLines = 32768;  // Miller lines
+// sets, the other streams filling the SIMDs a lane launch leaves free).  r06: with the
+// radix-2^28 lane kernels and their lazy combinations the lane form also wins from 8192 points
+// when two submissions are in flight (C3, 10 000 messages per launch: 835-855k -> 879k
+// messages/s in one box, profiles/r06/y_ab_lane_min.txt; C2's launches are 4096 or >= 65536).
+// One threshold for all three stages: g_lane_min (GBLS_LANE_MIN overrides it).
+constexpr uint32_t kLaneRegimeSets = 8192;
 // ... and Miller lines of up to this many pairs run on 16-lane DPP rows (bls_gang.h),
 // 16 x 4096 lanes being one wave per SIMD
 constexpr uint32_t kRowRegimeMax = 6144;

@@ -3,7 +3,7 @@
 // One DPP quad (4 lanes) per message: the doublings and additions run quad-cooperatively
 // (bls_gang.h); psi and the affine conversion run
 // redundantly in all four lanes and lane 0 stores.  Output: affine points (Miller-loop
-// input).  Launches of at least kLaneRegimeClear messages run one message per lane in two
+// input).  Launches of at least g_lane_min messages run one message per lane in two
 // kernels, one [|x|] chain each (k_h2c_clear_lane_a / _b, radix-2^28 by default: a quarter of
 // the instructions per message, the chip already full).
 #include "gbls_common.h"

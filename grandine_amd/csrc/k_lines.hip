@@ -9,7 +9,7 @@
 // gang_line_add_aff); lane q stores line components c with c % 4 == q.  Large batches
 // generate and consume the lines in event slices (the running point T kept in HBM
 // between slices), so the buffer holds a slice of events, not all 68.  Launches of at
-// least kLaneRegimeLines pairs run one pair per lane instead (k_lines_lane).
+// least g_lane_min pairs run one pair per lane instead (k_lines_lane).
 #include "gbls_common.h"
 #define GBLS_GANG_LINES
 #include "bls_gang.h"
