@@ -36,6 +36,11 @@ HD void f_one(fe2 &r) {
   for (int i = 0; i < 14; i++) r.c1.l[i] = 0;
 }
 HD bool f_is_zero(const fe2 &a) { return is_zero(a.c0) && is_zero(a.c1); }
+HD bool f_eq(const fe2 &a, const fe2 &b) {  // a, b normalized, < 4 p
+  fe2 d;
+  fe2_sub(d, a, b);
+  return f_is_zero(d);
+}
 
 // the lazy combinations (bls_field28.h) jac_dbl28 is written in
 HD void f_add_n(fe2 &r, const fe2 &a, const fe2 &b) { fe2_add_n(r, a, b); }
@@ -355,6 +360,27 @@ HD void g2a_load12(g2a28 &r, const g2a &src) {
   load12(r.y.c0, src.y.c0), load12(r.y.c1, src.y.c1);
 }
 
+// G2 membership in radix 2^28 (bls_curve.h g2_in_group: psi(P) == [x]P, x < 0) for an affine
+// point that is not infinity, in radix-2^28 form; the chain adds the affine base (mixed
+// additions), which may be parked in LDS by the caller (k_g2_check28)
+HD bool g2_in_group28(const g2a28 &b) {
+  g2j28 acc;
+  acc.x = b.x;
+  acc.y = b.y;
+  f_one(acc.z);
+  for (int i = 62; i >= 0; i--) {
+    jac_dbl(acc, acc);
+    if ((k::X_ABS >> i) & 1) jac_add_aff28<false>(acc, acc, b);
+  }
+  jac_neg(acc, acc);  // [x]P
+  g2j28 p, pp;
+  p.x = b.x;
+  p.y = b.y;
+  f_one(p.z);
+  g2_psi28(pp, p);
+  return jac_eq(pp, acc);
+}
+
 // h_eff P, the sequence of clear_cofactor_g2 (bls_hash.h, Budroni-Pintore): host tests of
 // the layer's G2 formulas (tests/native/host_harness.cpp)
 HD void clear_cofactor28(g2j28 &r, const g2j28 &p) {
@@ -399,6 +425,11 @@ HD void f_neg(fe &r, const fe &a) {
 }
 HD void f_one(fe &r) { r = K28_ONE; }
 HD bool f_is_zero(const fe &a) { return is_zero(a); }
+HD bool f_eq(const fe &a, const fe &b) {
+  fe d;
+  sub(d, a, b);
+  return is_zero(d);
+}
 
 HD void f_add_n(fe &r, const fe &a, const fe &b) { add_n(r, a, b); }
 HD void f_sub_n(fe &r, const fe &a, const fe &b) { sub(r, a, b); }

@@ -3,6 +3,7 @@
 
 #include "gbls_common.h"
 #include "bls_w4.h"
+#include "bls_curve28.h"
 
 namespace gbls {
 
@@ -86,6 +87,34 @@ __global__ void __launch_bounds__(WG) k_g2_check(const g2a *in, uint32_t n, int3
     st[i] = ok ? ST_SUCCESS : ST_NOT_IN_GROUP;
 }
 
+// the same with the membership chain in radix 2^28 (bls_curve28.h g2_in_group28: lazy
+// doublings, mixed additions of the base, which waits in LDS at an odd stride of 57 words)
+__global__ void __launch_bounds__(WG) k_g2_check28(const g2a *in, uint32_t n, int32_t *st,
+                                                   int accumulate) {
+  uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  struct g2a28_lds {
+    r28::g2a28 v;
+    uint32_t pad;
+  };
+  static_assert(sizeof(g2a28_lds) == 57 * 4, "odd LDS stride");
+  __shared__ g2a28_lds bl[WG];
+  const g2a a = in[i];
+  bool ok = aff_is_inf(a);
+  if (!ok && g2_on_curve(a)) {
+    r28::g2a28 &b = bl[threadIdx.x].v;
+    r28::g2a28 t;
+    r28::from_fp(t.x.c0, a.x.c0), r28::from_fp(t.x.c1, a.x.c1);
+    r28::from_fp(t.y.c0, a.y.c0), r28::from_fp(t.y.c1, a.y.c1);
+    b = t;
+    ok = r28::g2_in_group28(b);
+  }
+  if (accumulate)
+    st[i] = st[i] | (ok ? 0 : 1);
+  else
+    st[i] = ok ? ST_SUCCESS : ST_NOT_IN_GROUP;
+}
+
 __global__ void __launch_bounds__(WG) k_g1_compress(const g1a *in, uint32_t n, uint8_t *out) {
   uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
@@ -111,7 +140,11 @@ void launch_g2_decompress(hipStream_t st, const uint8_t *in, uint32_t n, g2a *ou
         in, n, out, status);
 }
 void launch_g2_check(hipStream_t st, const g2a *in, uint32_t n, int32_t *status, int accumulate) {
-  if (n) k_g2_check<<<nblk(n), WG, 0, st>>>(in, n, status, accumulate);
+  if (!n) return;
+  if (g_lane_r28)
+    k_g2_check28<<<nblk(n), WG, 0, st>>>(in, n, status, accumulate);
+  else
+    k_g2_check<<<nblk(n), WG, 0, st>>>(in, n, status, accumulate);
 }
 void launch_g1_compress(hipStream_t st, const g1a *in, uint32_t n, uint8_t *out) {
   if (n) k_g1_compress<<<nblk(n), WG, 0, st>>>(in, n, out);

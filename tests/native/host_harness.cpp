@@ -537,6 +537,28 @@ int h_r28_clear_check(const uint8_t *msg, uint32_t len) {
   return jac_eq(got, want) ? 1 : 0;
 }
 
+// G2 membership in radix 2^28 (bls_curve28.h g2_in_group28) against the engine's g2_in_group
+// for a message's cleared hash point (in G2) and its uncleared map output (on E2, not in G2):
+// 1 = both agree with the engine and the engine says (in, out)
+int h_r28_g2check(const uint8_t *msg, uint32_t len) {
+  fp2 u[2];
+  hash_to_field_g2(u, msg, len, dst_ref{POP, 43});
+  g2j q0, h;
+  map_to_g2(q0, u[0]);
+  clear_cofactor_g2(h, q0);
+  int ok = 1;
+  for (int k = 0; k < 2; k++) {
+    g2a a;
+    jac_to_aff(a, k == 0 ? h : q0);
+    r28::g2a28 b;
+    r28::from_fp(b.x.c0, a.x.c0), r28::from_fp(b.x.c1, a.x.c1);
+    r28::from_fp(b.y.c0, a.y.c0), r28::from_fp(b.y.c1, a.y.c1);
+    const bool want = g2_in_group(a), got = r28::g2_in_group28(b);
+    ok &= (got == want) && (want == (k == 0));
+  }
+  return ok;
+}
+
 // G1 [k]P in radix 2^28 (bls_curve28.h g1_mul_u64_w3_28 + g1s_from_jac28) against the engine's
 // g1_mul_u64_w3 + g1s_from_jac: the same point up to the scaled form's Fp factor (x / c, y / c
 // compared through cross products), for n seeded (P, k); 0 = all equal

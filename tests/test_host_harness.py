@@ -287,6 +287,16 @@ def test_radix28_g1_scalar_multiplication(H):
 
 
 
+def test_radix28_g2_subgroup_check(H):
+    """bls_curve28.h g2_in_group28 (k_g2_check28: psi(P) == [x]P with lazy doublings and mixed
+    additions of the affine base) equals the engine's g2_in_group: true for cleared hash points,
+    false for the uncleared map outputs (on E2, outside G2)."""
+    H.h_r28_g2check.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+    for i in range(4):
+        m = b"r28-g2check/%d" % i
+        assert H.h_r28_g2check(m, len(m)) == 1, i
+
+
 def test_radix28_lazy_doubling(H):
     """bls_curve28.h jac_dbl28 / jac_add28 / jac_add_aff28 (lazy combinations, weak reductions
     only where an output or a square's operand needs one) equal bls_curve.h's jac_dbl / jac_add /
