@@ -360,10 +360,40 @@ HD void g2a_load12(g2a28 &r, const g2a &src) {
   load12(r.y.c0, src.y.c0), load12(r.y.c1, src.y.c1);
 }
 
-// G2 membership in radix 2^28 (bls_curve.h g2_in_group: psi(P) == [x]P, x < 0) for an affine
-// point that is not infinity, in radix-2^28 form; the chain adds the affine base (mixed
-// additions), which may be parked in LDS by the caller (k_g2_check28)
-HD bool g2_in_group28(const g2a28 &b) {
+// 1/a (0 -> 0) through the engine's safegcd inversion (bls_field.h fp_inv): a < 16 p
+HD void inv(fe &r, const fe &a) {
+  fp t;
+  to_fp(t, a);
+  fp_inv(t, t);
+  from_fp(r, t);
+}
+// 1/a = conj(a) / N(a) (0 -> 0): a normalized, < 2.1 p
+HD void fe2_inv(fe2 &r, const fe2 &a) {
+  fe n, t;
+  sqr(n, a.c0);
+  sqr(t, a.c1);
+  add_n(n, n, t);
+  inv(n, n);
+  mul(r.c0, a.c0, n);
+  mul(t, a.c1, n);
+  fe z;
+#pragma unroll
+  for (int i = 0; i < 14; i++) z.l[i] = 0;
+  sub_r(r.c1, z, t);
+}
+// Jacobian -> affine, infinity -> (0, 0)
+HD void jac_to_aff28(g2a28 &r, const g2j28 &p) {
+  fe2 zi, zi2, zi3;
+  fe2_inv(zi, p.z);
+  fe2_sqr(zi2, zi);
+  fe2_mul(zi3, zi2, zi);
+  fe2_mul(r.x, p.x, zi2);
+  fe2_mul(r.y, p.y, zi3);
+}
+// [|x|] b for an affine base ((0, 0): infinity, whose chain runs on garbage and is dropped): 63
+// lazy doublings and 5 mixed additions -- 256 VGPRs, no scratch, so two waves per SIMD
+// (tools/ubench/occ28_bench.hip).  b may live in LDS.
+HD void g2_xabs_aff28(g2j28 &r, const g2a28 &b) {
   g2j28 acc;
   acc.x = b.x;
   acc.y = b.y;
@@ -372,13 +402,65 @@ HD bool g2_in_group28(const g2a28 &b) {
     jac_dbl(acc, acc);
     if ((k::X_ABS >> i) & 1) jac_add_aff28<false>(acc, acc, b);
   }
+  if (f_is_zero(b.x) && f_is_zero(b.y)) jac_set_inf(acc);
+  r = acc;
+}
+HD void g2j_of_aff28(g2j28 &r, const g2a28 &a) {
+  r.x = a.x;
+  r.y = a.y;
+  f_one(r.z);
+  if (f_is_zero(a.x) && f_is_zero(a.y)) jac_set_inf(r);
+}
+
+// G2 membership in radix 2^28 (bls_curve.h g2_in_group: psi(P) == [x]P, x < 0) for an affine
+// point that is not infinity, in radix-2^28 form; the affine base may be parked in LDS by the
+// caller (k_g2_check28)
+HD bool g2_in_group28(const g2a28 &b) {
+  g2j28 acc;
+  g2_xabs_aff28(acc, b);
   jac_neg(acc, acc);  // [x]P
   g2j28 p, pp;
-  p.x = b.x;
-  p.y = b.y;
-  f_one(p.z);
+  g2j_of_aff28(p, b);
   g2_psi28(pp, p);
   return jac_eq(pp, acc);
+}
+
+// The lane-regime cofactor clearing in stages (k_h2c_clear.hip), with both [|x|] chains on
+// affine bases (g2_xabs_aff28, their own two-waves-per-SIMD kernel):
+//   pre:   P = Q0 + Q1, affine
+//   chain: X1 = [|x|] P
+//   mid:   t1 = -X1 = [x]P;  t2 = t1 + psi(P) (affine);  T = X1 - P + psi^2(2P) - psi(P)
+//   chain: X2 = [|x|] t2
+//   post:  h = T - X2 = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)   (clear_cofactor_g2)
+HD void clear_mid28(g2a28 &t2a, g2j28 &T, const g2a28 &pa, const g2j28 &x1) {
+  g2j28 p, t1, t2, v;
+  g2j_of_aff28(p, pa);
+  jac_neg(t1, x1);  // [x]P
+  g2_psi28(t2, p);
+  jac_add(t2, t2, t1);  // t1 + psi(P)
+  jac_to_aff28(t2a, t2);
+  jac_neg(v, p);
+  jac_add(T, x1, v);  // - t1 - P
+  jac_dbl(v, p);
+  g2_psi2_28(v, v);
+  jac_add(T, T, v);  // + psi^2(2P)
+  g2_psi28(v, p);
+  jac_neg(v, v);
+  jac_add(T, T, v);  // - psi(P)
+}
+HD void clear_post28(g2j28 &h, const g2j28 &x2, const g2j28 &T) {
+  jac_neg(h, x2);
+  jac_add(h, h, T);
+}
+// the stages in sequence (host tests)
+HD void clear_cofactor28_staged(g2j28 &r, const g2j28 &p) {
+  g2a28 pa, t2a;
+  g2j28 x1, x2, T;
+  jac_to_aff28(pa, p);
+  g2_xabs_aff28(x1, pa);
+  clear_mid28(t2a, T, pa, x1);
+  g2_xabs_aff28(x2, t2a);
+  clear_post28(r, x2, T);
 }
 
 // h_eff P, the sequence of clear_cofactor_g2 (bls_hash.h, Budroni-Pintore): host tests of

@@ -233,6 +233,79 @@ __global__ void __launch_bounds__(WG) k_h2c_clear_lane_b28(const g2j *Q, uint32_
   H[i] = o;
 }
 
+// The staged form (GBLS_CLEAR_STAGED=1, off by default; bls_curve28.h clear_mid28): both
+// [|x|] chains run on AFFINE bases in their own kernel, k_h2c_chain28, whose 63 lazy doublings
+// and 5 mixed additions fit 256 VGPRs without scratch: two waves per SIMD, so a chain launch
+// shares its SIMDs with the other in-flight submission's waves (the one-kernel chains above take
+// 256 VGPRs + ~250 AGPRs for the Jacobian base's full additions).  The affine conversions cost
+// one safegcd inversion each (pre, mid).  Per message the Q slots carry, in radix-2^28 limbs:
+//   pre:   Q[2i] = P = Q0 + Q1 (affine x, y)
+//   chain: Q[2i+1] = X1 = [|x|] P
+//   mid:   Q[2i] = t2 = [x]P + psi(P) (affine), Q[2i+1] = T = X1 - P + psi^2(2P) - psi(P)
+//   chain: Q[2i] = X2 = [|x|] t2
+//   post:  H[i] = affine(T - X2), engine form
+// Measured (profiles/r06/y_ab_clear_staged.txt, one box): C2 4.57-4.72M against 4.63-4.69M, C3
+// 795-824k against 827-855k.  A chain launch of one submission is 1024 waves, one per SIMD, and
+// the other submission's kernels take 512 registers per wave, so the second wave slot is rarely
+// used, while the affine conversions and the extra launches cost.  Kept as a knob.
+__device__ __forceinline__ g2a &q_aff(g2j &slot) { return *reinterpret_cast<g2a *>(&slot); }
+__global__ void __launch_bounds__(WG) k_h2c_clear_pre28(g2j *Q, uint32_t n) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  r28::g2j28 p, q;
+  r28::g2j_in(p, Q[2 * i]);
+  r28::g2j_in(q, Q[2 * i + 1]);
+  jac_add(p, p, q);
+  r28::g2a28 a;
+  r28::jac_to_aff28(a, p);
+  r28::g2a_store12(q_aff(Q[2 * i]), a);
+}
+struct g2a28_lds {
+  r28::g2a28 v;
+  uint32_t pad;
+};
+static_assert(sizeof(g2a28_lds) == 57 * 4, "odd LDS stride");
+template <int SRC, int DST>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_h2c_chain28(g2j *Q, uint32_t n) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  __shared__ g2a28_lds bl[WG];
+  r28::g2a28 &b = bl[threadIdx.x].v;
+  {
+    r28::g2a28 t;
+    r28::g2a_load12(t, q_aff(Q[2 * i + SRC]));
+    b = t;
+  }
+  r28::g2j28 h;
+  r28::g2_xabs_aff28(h, b);
+  r28::g2j_store12(Q[2 * i + DST], h);
+}
+__global__ void __launch_bounds__(WG) k_h2c_clear_mid28(g2j *Q, uint32_t n) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  r28::g2a28 pa, t2a;
+  r28::g2j28 x1, T;
+  r28::g2a_load12(pa, q_aff(Q[2 * i]));
+  r28::g2j_load12(x1, Q[2 * i + 1]);
+  r28::clear_mid28(t2a, T, pa, x1);
+  r28::g2a_store12(q_aff(Q[2 * i]), t2a);
+  r28::g2j_store12(Q[2 * i + 1], T);
+}
+__global__ void __launch_bounds__(WG) k_h2c_clear_post28(const g2j *Q, uint32_t n, g2a *H) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  r28::g2j28 x2, T, h;
+  r28::g2j_load12(x2, Q[2 * i]);
+  r28::g2j_load12(T, Q[2 * i + 1]);
+  r28::clear_post28(h, x2, T);
+  g2j e;
+  r28::g2j_out(e, h);
+  g2a o;
+  jac_to_aff(o, e);
+  H[i] = o;
+}
+
 // one wave per message (bls_w4.h: four row-distributed products per round), the smallest
 // launches: Q0 + Q1, the cofactor clearing and the affine conversion at ~0.5 us per round
 template <bool X>
@@ -279,8 +352,15 @@ void launch_h2c_clear(hipStream_t st, const g2j *Q, uint32_t n, g2a *H) {
   else if (n >= g_lane_min) {
     // Q is a scratch of the call (the map's output); its two slots per message carry the
     // points between the two chains
-    if (g_lane_r28) {
-      k_h2c_clear_lane_a28<<<nblk(n), WG, 0, st>>>(const_cast<g2j *>(Q), n);
+    g2j *Qw = const_cast<g2j *>(Q);
+    if (g_lane_r28 && g_clear_staged) {
+      k_h2c_clear_pre28<<<nblk(n), WG, 0, st>>>(Qw, n);
+      k_h2c_chain28<0, 1><<<nblk(n), WG, 0, st>>>(Qw, n);
+      k_h2c_clear_mid28<<<nblk(n), WG, 0, st>>>(Qw, n);
+      k_h2c_chain28<0, 0><<<nblk(n), WG, 0, st>>>(Qw, n);
+      k_h2c_clear_post28<<<nblk(n), WG, 0, st>>>(Q, n, H);
+    } else if (g_lane_r28) {
+      k_h2c_clear_lane_a28<<<nblk(n), WG, 0, st>>>(Qw, n);
       k_h2c_clear_lane_b28<<<nblk(n), WG, 0, st>>>(Q, n, H);
     } else {
       k_h2c_clear_lane_a<<<nblk(n), WG, 0, st>>>(const_cast<g2j *>(Q), n);

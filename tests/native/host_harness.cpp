@@ -530,11 +530,14 @@ int h_r28_clear_check(const uint8_t *msg, uint32_t len) {
   map_to_g2(q1, u[1]);
   jac_add(q0, q0, q1);
   clear_cofactor_g2(want, q0);
-  r28::g2j28 a, h;
+  r28::g2j28 a, h, hs;
   r28::g2j_in(a, q0);
   r28::clear_cofactor28(h, a);
   r28::g2j_out(got, h);
-  return jac_eq(got, want) ? 1 : 0;
+  g2j gs;  // the lane kernels' staged form (affine chain bases)
+  r28::clear_cofactor28_staged(hs, a);
+  r28::g2j_out(gs, hs);
+  return jac_eq(got, want) && jac_eq(gs, want) ? 1 : 0;
 }
 
 // G2 membership in radix 2^28 (bls_curve28.h g2_in_group28) against the engine's g2_in_group

@@ -304,12 +304,14 @@ def test_bucket_msm_parity_subprocess():
 
 
 @pytest.mark.parametrize("knobs", [["GBLS_ML_DMA=1"], ["GBLS_ML_R28=0"], ["GBLS_LANE_R28=0"], ["GBLS_ML_KARA=1"],
-                                   ["GBLS_LANE_MIN=1"]],
-                         ids=["ml-lds-dma", "ml-radix32", "lanes-radix32", "ml-karatsuba", "lanes-everywhere"])
+                                   ["GBLS_LANE_MIN=1"], ["GBLS_LANE_MIN=1", "GBLS_CLEAR_STAGED=1"]],
+                         ids=["ml-lds-dma", "ml-radix32", "lanes-radix32", "ml-karatsuba", "lanes-everywhere",
+                              "clear-staged"])
 def test_kernel_variants_subprocess(knobs):
     """The non-default kernel forms an operator can select (k_ml_group28 with the line staged
     in LDS by DMA loads; the 32-bit-limb k_ml_group; the 32-bit-limb line / cofactor lanes; the
-    lane forms at every launch size above the W4 regime, partial waves included):
+    lane forms at every launch size above the W4 regime, partial waves included; the same with
+    the staged cofactor clearing, GBLS_CLEAR_STAGED=1):
     golden multi_verify verdicts, 4096-set batches equal to the C oracle's, and a 4-segment
     batch that flags exactly its corrupted segment (tests/gpu_knobs.py, its own engine)."""
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_knobs.py")] + knobs,
