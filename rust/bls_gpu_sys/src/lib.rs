@@ -278,6 +278,51 @@ pub fn g2_aggregate(points: &[P2]) -> EngineResult<P2> {
     status(rc).map(|()| out)
 }
 
+/// f4: `Signature::try_from` of many 96-byte encodings in one call: per input the point or the
+/// decoder's BLST_ERROR (on-curve check only, as `RawSignature::uncompress`).
+pub fn g2_decompress_many(bytes: &[[u8; 96]]) -> EngineResult<Vec<Result<P2, BLST_ERROR>>> {
+    let n = bytes.len();
+    if n == 0 {
+        return Ok(Vec::new());
+    }
+    let mut out = vec![P2::default(); n];
+    let mut statuses = vec![ffi::GBLS_BAD_ENCODING; n];
+    // SAFETY: `bytes` is a live slice of n 96-byte encodings; n output points and n statuses.
+    let rc = unsafe { ffi::gbls_g2_decompress(bytes.as_ptr(), n, out.as_mut_ptr(), statuses.as_mut_ptr()) };
+    status(rc)?;
+    Ok(out
+        .into_iter()
+        .zip(statuses)
+        .map(|(point, s)| if s == ffi::GBLS_SUCCESS { Ok(point) } else { Err(blst_error(s)) })
+        .collect())
+}
+
+/// f4: per segment s the sum of `points[offsets[s] .. offsets[s + 1]]`, every segment in one
+/// submission (`Signature::aggregate_in_place` over an op-pool batch).  `offsets` starts at 0,
+/// strictly increases (no empty segment) and ends at `points.len()`; otherwise an argument error.
+pub fn g2_aggregate_segments(points: &[P2], offsets: &[u32]) -> EngineResult<Vec<P2>> {
+    let nseg = offsets.len().checked_sub(1).ok_or(EngineError::Argument)?;
+    let spans_points = usize::try_from(offsets[nseg]).is_ok_and(|end| end == points.len());
+    if offsets[0] != 0 || !spans_points || offsets.windows(2).any(|w| w[1] <= w[0]) {
+        return Err(EngineError::Argument);
+    }
+    if nseg == 0 {
+        return Ok(Vec::new());
+    }
+    let mut out = vec![P2::default(); nseg];
+    let mut statuses = vec![ffi::GBLS_AGGR_TYPE_MISMATCH; nseg];
+    // SAFETY: `points` holds offsets[nseg] points and `offsets` nseg + 1 entries (checked above);
+    // nseg output points and nseg statuses.
+    let rc = unsafe {
+        ffi::gbls_g2_aggregate_segments(points.as_ptr(), offsets.as_ptr(), nseg, out.as_mut_ptr(), statuses.as_mut_ptr())
+    };
+    status(rc)?;
+    if statuses.iter().any(|&s| s != ffi::GBLS_SUCCESS) {
+        return Err(EngineError::Argument);
+    }
+    Ok(out)
+}
+
 /// a6: `Signature::verify` semantics (signature subgroup check, infinite key rejected).
 pub fn verify(signature: &P2, message: &[u8], key: &P1) -> EngineResult<bool> {
     // SAFETY: `message` is a live slice of `message.len()` bytes; single points by reference.

@@ -146,6 +146,48 @@ pub fn multi_verify_compressed_indexed(
     })
 }
 
+/// f4: `aggregate_in_place` of many message signatures into many aggregates in two engine calls
+/// (the op-pool loops, `operation_pools/src/sync_committee_agg_pool/pool.rs:90-115,159-192`):
+/// `additions[i] = (k, bytes)` adds the signature `bytes` to `bases[k]`, in order.  The encodings
+/// are decoded in one call (`Signature::try_from` semantics) and every aggregate's sum is formed
+/// in one `gbls_g2_aggregate_segments` submission.  When an encoding does not decode, only the
+/// additions before the FIRST such one are summed and `Err((i, error))` names it, which is the
+/// state the reference's `try_into()?` loop stops in.
+/// `None`: no engine verdict (absent engine, engine error) -- `bases` is untouched and the
+/// caller runs its blst loop.
+#[must_use]
+pub fn aggregate_into(
+    bases: &mut [Signature],
+    additions: &[(usize, crate::SignatureBytes)],
+) -> Option<Result<(), (usize, crate::Error)>> {
+    if additions.iter().any(|(k, _)| *k >= bases.len()) {
+        return None;
+    }
+    let encodings = additions.iter().map(|(_, bytes)| bytes.to_fixed_bytes()).collect::<Vec<[u8; 96]>>();
+    let decoded = counted(|| bls_gpu_sys::g2_decompress_many(&encodings))?;
+    let first_bad = decoded.iter().position(Result::is_err);
+    let upto = first_bad.unwrap_or(additions.len());
+    let mut segments = bases.iter().map(|base| vec![signature_point(base)]).collect::<Vec<Vec<P2>>>();
+    for ((k, _), point) in additions[..upto].iter().zip(&decoded) {
+        segments[*k].push(*point.as_ref().ok()?);
+    }
+    let mut offsets = vec![0_u32];
+    for segment in &segments {
+        offsets.push(offsets[offsets.len() - 1] + u32::try_from(segment.len()).ok()?);
+    }
+    let points = segments.concat();
+    let sums = counted(|| bls_gpu_sys::g2_aggregate_segments(&points, &offsets))?;
+    // every sum converted before any base is replaced: a failure leaves `bases` as it was
+    let raws = sums.iter().map(|sum| bls_gpu_sys::signature_of_p2(sum).ok()).collect::<Option<Vec<_>>>()?;
+    for (base, raw) in bases.iter_mut().zip(raws) {
+        *base = Signature::from(raw);
+    }
+    Some(match first_bad {
+        None => Ok(()),
+        Some(i) => Err((i, crate::Error::DecompressionFailed(decoded[i].err()?))),
+    })
+}
+
 /// f1: the engine's copy of the validator registry (device-resident keys, decompressed once).
 ///
 /// Validator indices name the same key on every fork only up to the finalized state: a deposit

@@ -422,3 +422,55 @@ def test_registry_mirror_indexed_finish(G, L, F, REF):
         mv.finish(rands)
     assert mv.last_path == "points"
     B.Registry.forget()
+
+
+def test_sync_pool_aggregation_in_one_submission(G):
+    """f4: the sync-committee pool's aggregate_messages (pool.rs:142-195) through
+    grandine_amd.pools -- the messages' signatures decompressed in one call, every aggregate's sum
+    in one gbls_g2_aggregate_segments submission -- against the reference loop run with the
+    oracle's point decoding and additions: equal bits and equal aggregate signatures, clean and
+    with a message whose signature does not decode (the reference returns there, that bit set)."""
+    from grandine_amd import bls as B
+    from grandine_amd import pools
+    from oracle import bls12_381 as O
+    sks = [O.interop_secret_key(i).to_bytes(32, "big") for i in range(6)]
+    sigs = [s.to_bytes() for s in B.sign_batch(sks, [bytes([0x60 + i]) * 32 for i in range(6)])]
+    bad = bytearray(sigs[3])
+    bad[0] &= 0x7f  # no compression flag: a 96-byte input that does not decode
+    assert O.g2_decompress(bytes(bad))[1] is None
+    size = 8
+    for with_bad in (False, True):
+        msgs = [([0], sigs[0]), ([1], sigs[1]), ([2, 3], sigs[2]), ([6], sigs[4])]
+        if with_bad:
+            msgs.insert(3, ([4], bytes(bad)))
+        base = B.Signature.try_from(sigs[5])
+        aggs = [pools.Aggregate(size, signature=base, bits=[i == 1 for i in range(size)]), pools.Aggregate(size)]
+        # the reference loop with the oracle
+        want_bits = [list(a.bits) for a in aggs]
+        want_pts = [O.g2_decompress(bytes(sigs[5]))[1], None]
+        err = None
+        for positions, sb in msgs:
+            for pos in positions:
+                for k in range(2):
+                    if want_bits[k][pos]:
+                        continue
+                    want_bits[k][pos] = True
+                    st, pt = O.g2_decompress(bytes(sb))
+                    if pt is None:
+                        err = st
+                        break
+                    want_pts[k] = pt if want_pts[k] is None else O.g2_add(want_pts[k], pt)
+                if err is not None:
+                    break
+            if err is not None:
+                break
+        raised = None
+        try:
+            pools.aggregate_messages(aggs, msgs, size)
+        except B.DecompressionFailed as e:
+            raised = e
+        assert (raised is not None) == with_bad == (err is not None)
+        assert [a.bits for a in aggs] == want_bits
+        for a, pt in zip(aggs, want_pts):
+            want = O.g2_compress(pt) if pt is not None else bytes([0xc0]) + bytes(95)
+            assert bytes(a.signature.to_bytes()) == want

@@ -200,7 +200,8 @@ def test_safe_wrappers_call_the_header_entry_points():
                 "verify": "gbls_verify", "fast_aggregate_verify": "gbls_fast_aggregate_verify",
                 "multi_verify": "gbls_multi_verify", "multi_verify_compressed": "gbls_multi_verify_compressed_ex",
                 "multi_verify_bisect": "gbls_multi_verify_bisect", "engine": "gbls_init",
-                "verify_batch_compressed": "gbls_verify_batch_compressed", "set_policy": "gbls_set_policy"}
+                "verify_batch_compressed": "gbls_verify_batch_compressed", "set_policy": "gbls_set_policy",
+                "g2_decompress_many": "gbls_g2_decompress", "g2_aggregate_segments": "gbls_g2_aggregate_segments"}
     for w, entry in wrappers.items():
         body = fns[w]
         m = re.search(r"ffi::%s\((.*?)\)\s*\}?;?\n" % entry, body, flags=re.S)
@@ -350,3 +351,28 @@ def test_registry_mirror_names_slots_in_finish():
     args = [a.strip() for a in m.group(1).split(",") if a.strip()]
     assert args[2] == "ptr::null()" and args[3] == "indices.as_ptr()" and args[4] == "index_offsets.as_ptr()"
     assert "status(rc)?" in fns["registry_set"] and "ffi::gbls_registry_set(first, keys.as_ptr()" in fns["registry_set"]
+
+
+def test_sync_pool_aggregates_in_one_submission():
+    """f4 (VERDICT r05 "missing 1"): the sync-committee pool's message loops
+    (operation_pools/src/sync_committee_agg_pool/pool.rs:90-115, 159-192) plan their additions and
+    hand them to bls::gpu::aggregate_into (one batched decode + one segmented sum); the reference
+    loops stay as the no-verdict fallback; a decode failure stops the sums where the reference's
+    `try_into()?` returns."""
+    pool = _strip_comments(open(os.path.join(PATCH, "sync_committee_pool.rs")).read())
+    gpu = _strip_comments(open(os.path.join(PATCH, "gpu.rs")).read())
+    agg = _rust_fns(gpu)["aggregate_into"]
+    assert "bls_gpu_sys::g2_decompress_many(" in agg and "bls_gpu_sys::g2_aggregate_segments(" in agg
+    assert "position(Result::is_err)" in agg and "additions[..upto]" in agg
+    # bases are replaced only after every sum converted
+    assert agg.index("collect::<Option<Vec<_>>>()?") < agg.index("*base = Signature::from(raw)")
+    for fn in ("add_sync_committee_contribution", "aggregate_messages"):
+        body = _rust_fns(pool.replace("pub async fn", "pub fn"))[fn]
+        assert "plan_additions(" in body and "add_on_engine(" in body, fn
+        # the reference loop, with its per-message decode, is the fallback
+        assert ".aggregate_in_place(message.signature.try_into()?)" in body, fn
+        assert "lookup_error" in body, fn
+    eng = pool.split("fn add_on_engine", 1)[1].split("\npub async fn", 1)[0]
+    assert "bls::gpu::aggregate_into(" in eng
+    # no verdict: every planned bit cleared; a failure: the bits after it cleared
+    assert "for a in plan {" in eng and "&plan[i + 1..]" in eng
