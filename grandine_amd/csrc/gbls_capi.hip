@@ -57,6 +57,7 @@ uint32_t gbls::g_ml_kara = 0;
 uint32_t gbls::g_lane_r28 = 1;
 uint32_t gbls::g_lane_min = gbls::kLaneRegimeSets;
 uint32_t gbls::g_clear_staged = 0;
+uint32_t gbls::g_map_rows_max = 2048;
 
 namespace {
 
@@ -582,6 +583,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
     if (const char *e = std::getenv("GBLS_ML_XCD")) g_ml_xcd = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LANE_R28")) g_lane_r28 = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_CLEAR_STAGED")) g_clear_staged = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GBLS_MAP_ROWS_MAX")) g_map_rows_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_LANE_MIN")) g_lane_min = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char *e = std::getenv("GBLS_CU_SPLIT_MAX"))
       g.cu_split_max = (uint32_t)std::strtoul(e, nullptr, 10);

@@ -52,6 +52,7 @@ extern uint32_t g_ml_dma;                // k_ml_group28: line staged in LDS by 
 extern uint32_t g_ml_xcd;                // k_ml_group: XCD-grouped block order (GBLS_ML_XCD)
 extern uint32_t g_lane_r28;              // lane-regime clearing / lines in radix 2^28 (GBLS_LANE_R28)
 extern uint32_t g_clear_staged;          // lane clearing in five stages, chains at two waves per SIMD (GBLS_CLEAR_STAGED=1; off)
+extern uint32_t g_map_rows_max;          // hash_to_G2 maps of up to this many field elements on 16-lane rows (GBLS_MAP_ROWS_MAX)
 extern uint32_t g_lane_min;              // launches of at least this many points take the lane regime (GBLS_LANE_MIN)
 // line-coefficient buffer bound per submission (19.6 KB per pair: 4 GB = 214k pairs,
 // a C5 shard of 131 072 sets unsliced; tiny next to 288 GB of HBM): above it the Miller

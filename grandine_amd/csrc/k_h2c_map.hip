@@ -41,15 +41,12 @@ __global__ void __launch_bounds__(WG) k_h2c_map_row(const fp2 *U, uint32_t nu, g
   if ((threadIdx.x & 15) == 0) Q[i] = q;
 }
 
-// field elements up to this many take the row form (16 lanes each: 512 waves at the limit)
-#ifndef GBLS_MAP_ROWS_MAX
-#define GBLS_MAP_ROWS_MAX 2048
-#endif
-constexpr uint32_t kMapRowsMax = GBLS_MAP_ROWS_MAX;
+// field elements up to g_map_rows_max (2048 unless GBLS_MAP_ROWS_MAX is set) take the row form
+// (16 lanes each: 512 waves at 2048)
 
 void launch_h2c_map(hipStream_t st, const fp2 *U, uint32_t nu, g2j *Q) {
   if (!nu) return;
-  if (nu <= kMapRowsMax)
+  if (nu <= g_map_rows_max)
     (nblk((size_t)nu * 16) <= w4::kExclusiveMaxWaves ? k_h2c_map_row<true> : k_h2c_map_row<false>)<<<
         nblk((size_t)nu * 16), WG, 0, st>>>(U, nu, Q);
   else
