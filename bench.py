@@ -171,6 +171,8 @@ def main():
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="C4 on one GPU: verify only rank 0's committees of an N-way split (its per-GPU "
                          "shard shape) and report the node rate that shape predicts (DESIGN.md 5)")
+    ap.add_argument("--load-threads", type=int, default=16,
+                    help="C1: gossip threads of the concurrent window and of the block-under-load legs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stages", action="store_true",
                     help="no per-stage HIP-event timing in the timed region (roofline stage times absent)")
@@ -704,7 +706,7 @@ def bench_c1(args, L, G, F, np):
         assert L.gbls_multi_verify(gm, gs, gp, r64, 64) == G.SUCCESS
         glat.append(time.perf_counter() - t)
     # 16 threads for a fixed 2 s window (steady state: the calls completed inside it count)
-    nthr, window = 16, 2.0
+    nthr, window = args.load_threads, 2.0
     errs = []
     done_calls = [0] * nthr
     go = threading.Event()
@@ -800,7 +802,7 @@ def bench_c1(args, L, G, F, np):
                 "block_priority_p99_ms": round(lat_prio[min(len(lat_prio) - 1, int(len(lat_prio) * 0.99))] * 1e3, 3),
                 "no_priority_p50_ms": round(lat_noprio[len(lat_noprio) // 2] * 1e3, 3),
                 "no_priority_p99_ms": round(lat_noprio[min(len(lat_noprio) - 1, int(len(lat_noprio) * 0.99))] * 1e3, 3),
-                "load": "16 threads x 64-set gbls_multi_verify in a loop"},
+                "load": "%d threads x 64-set gbls_multi_verify in a loop" % nthr},
             "gossip64_under_back_to_back_blocks": {
                 "p50_ms": round(glat_b[len(glat_b) // 2] * 1e3, 3),
                 "p99_ms": round(glat_b[min(len(glat_b) - 1, int(len(glat_b) * 0.99))] * 1e3, 3),
