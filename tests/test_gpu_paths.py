@@ -493,10 +493,16 @@ def test_c5_full_2pow20_sliced_accept_and_reject(G, L, F, REF, registry):
     bad_s[192 * j:192 * (j + 2)] = sigs[192 * (j + 1):192 * (j + 2)] + sigs[192 * j:192 * (j + 1)]
     bad_s = bytes(bad_s)
     assert L.gbls_multi_verify_indexed(msgs, bad_s, idx_c, None, u64(rands), n) == G.VERIFY_FAIL
-    for (m_, s_, at) in ((bad_m, sigs, 700001 - 1000), (msgs, bad_s, n - 2048)):
+    # the C oracle and the engine on 2048-set slices of the same bytes: a clean slice (accept,
+    # so the full-size accept above is not pinned by device-signed data alone) and the slice
+    # around each corruption (reject)
+    for (m_, s_, at, want) in ((msgs, sigs, 300000, 1), (bad_m, sigs, 700001 - 1000, 0), (msgs, bad_s, n - 2048, 0)):
         b, e = at, at + 2048
         pk_pts = F.public_keys([sks[int(i)] for i in idx[b:e]])
-        assert REF.ref_multi_verify(m_[32 * b:32 * e], s_[192 * b:192 * e], pk_pts, u64(rands[b:e]), e - b, 16) == 0
+        assert REF.ref_multi_verify(m_[32 * b:32 * e], s_[192 * b:192 * e], pk_pts, u64(rands[b:e]), e - b, 16) == want
+        sl = np.ascontiguousarray(idx[b:e])
+        assert L.gbls_multi_verify_indexed(m_[32 * b:32 * e], s_[192 * b:192 * e], sl.ctypes.data_as(ctypes.c_void_p),
+                                           None, u64(rands[b:e]), e - b) == (G.SUCCESS if want else G.VERIFY_FAIL)
 
 
 # ------------------------------------------------------------------ C3

@@ -1,3 +1,4 @@
+# (Needs the build that had the GBLS_BLOCK_QUEUE knob, removed after this A/B: profiles/r06/zz_ab_block_queue.txt.)
 # Same-box A/B of GBLS_BLOCK_QUEUE (block import on one high-priority stream that keeps a hardware
 # queue to itself; normal contexts created on demand take their main chain low): the C1 leg
 # (idle block, block under 16-thread gossip load) R times per mode, the default C2 line once.
