@@ -474,3 +474,38 @@ def test_sync_pool_aggregation_in_one_submission(G):
         for a, pt in zip(aggs, want_pts):
             want = O.g2_compress(pt) if pt is not None else bytes([0xc0]) + bytes(95)
             assert bytes(a.signature.to_bytes()) == want
+
+
+def test_reference_unit_cases(G, L, REF):
+    """The reference's own unit tests of the path, restated on the engine: bls/src/signature.rs:
+    147-172 (sk = 32 x '?', message "foo": verify accepts the correct triple, rejects
+    PublicKey::default() and Signature::default()) and helper_functions/src/verifier.rs:446-461
+    (MultiVerifier::finish with 0 signatures and with 1, message H256::default()); the key and the
+    accept are checked against the C oracle too."""
+    from grandine_amd import bls as B, verifier as V
+    sk = B.SecretKey.try_from(b"?" * 32)
+    pk = sk.to_public_key()
+    out = ctypes.create_string_buffer(96)
+    REF.ref_sk_to_pk(b"?" * 32, out)
+    assert out.raw == pk.raw
+    sig = sk.sign(b"foo")
+    assert sig.verify(b"foo", pk)
+    assert REF.ref_verify(sig.raw, b"foo", 3, pk.raw) == 1
+    assert not sig.verify(b"foo", B.PublicKey.default())
+    assert not B.Signature.default().verify(b"foo", pk)
+    assert not sig.verify(b"fop", pk) and REF.ref_verify(sig.raw, b"fop", 3, pk.raw) == 0
+    V.MultiVerifier().finish()
+    mv = V.MultiVerifier()
+    m = bytes(32)
+    mv.verify_singular(m, sk.sign(m).to_bytes(), B.CachedPublicKey(pk.to_bytes()), V.SignatureKind.Block)
+    mv.finish()
+    # helper_functions/src/predicates.rs:757-865, the signature part: the 2-key aggregate of sks
+    # 32 x '?' and 32 x '!' verifies (the attestation's SSZ signing root is outside the path: a
+    # fixed 32-byte message stands for it), and all-zero public key bytes do not decompress
+    sk2 = B.SecretKey.try_from(b"!" * 32)
+    root = bytes([0xff]) * 32
+    agg = sk.sign(root).aggregate(sk2.sign(root))
+    assert agg.fast_aggregate_verify(root, [pk, sk2.to_public_key()])
+    assert not agg.fast_aggregate_verify(root, [pk])
+    with pytest.raises(B.DecompressionFailed):
+        B.PublicKey.try_from(bytes(48))
