@@ -91,25 +91,36 @@ __global__ void __launch_bounds__(64) k_mv_g2mul_w4(const g2a *sigs, const uint6
   w4::store_jac(c, R + t, acc);
 }
 
-// level 2 on one wave per segment (bls_w4.h): the segment's chunk partials in sequence, the
-// 2^32 shift of the high half (32 doublings) and the affine conversion, ~0.3 ms instead of the
-// quads' ~0.6 ms (their one-lane inversion dominates)
+// level 2 on one workgroup of kFinalW4Waves waves per segment (bls_w4.h, one wave per SIMD):
+// wave w sums the segment's chunk partials q = w, w + NW, ... (a low- and a high-half
+// accumulator), a two-level tree joins the waves through LDS (the row-form registers as they
+// are), then wave 0 applies the 2^32 shift of the high half (32 doublings) and stores S --
+// ~0.3 ms instead of the quads' ~0.6 ms (their one-lane inversion dominates).  The serial
+// additions over the chunk partials drop from one per chunk (16 for a 2048-set segment) to
+// ceil(chunks / NW) + 2 per half: the signature side sets the join of C4-shaped submissions
+// (profiles/r06/zz_c4_join_wait.txt).  S is the same group element (only its Jacobian scale
+// changes, which the final exponentiation removes from its lines).
+constexpr int kFinalW4Waves = 4;
 template <bool X>
-__global__ void __launch_bounds__(64) k_g2sum_final_w4(const g2j *part, const int32_t *part_err,
-                                                       const uint32_t *chunks, const uint32_t *seg_chunk,
-                                                       const uint32_t *seg_off, uint32_t nseg, uint32_t n,
-                                                       int empty_is_error, g1s *P, g2a *H,
-                                                       int32_t *seg_err, g2j *Sj) {
+__global__ void __launch_bounds__(64 * kFinalW4Waves) k_g2sum_final_w4(const g2j *part, const int32_t *part_err,
+                                                                       const uint32_t *chunks, const uint32_t *seg_chunk,
+                                                                       const uint32_t *seg_off, uint32_t nseg, uint32_t n,
+                                                                       int empty_is_error, g1s *P, g2a *H,
+                                                                       int32_t *seg_err, g2j *Sj) {
   if constexpr (X) w4::exclusive_simd();
+  constexpr int NW = kFinalW4Waves;
+  __shared__ uint32_t sh[NW / 2][12 * 64];  // a sending wave's lo and hi, word k of lane l at k * 64 + l
+  __shared__ int32_t sh_err[NW];
   const uint32_t s = blockIdx.x;
-  if (s >= nseg) return;
+  if (s >= nseg) return;  // block-uniform
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   w4::Ctx c;
   w4::init(c);
   w4::J lo, hi;
   w4::set_inf(c, lo);
   w4::set_inf(c, hi);
   int32_t err = 0;
-  for (uint32_t q = seg_chunk[s]; q < seg_chunk[s + 1]; q++) {
+  for (uint32_t q = seg_chunk[s] + w; q < seg_chunk[s + 1]; q += NW) {
     w4::J v;
     w4::load(c, v, part[q]);
     if (chunks[4 * q + 1] == 0)
@@ -118,6 +129,33 @@ __global__ void __launch_bounds__(64) k_g2sum_final_w4(const g2j *part, const in
       w4::add(c, hi, hi, v);
     err |= part_err[q];
   }
+  if (lane == 0) sh_err[w] = err;
+  for (uint32_t width = NW / 2; width > 0; width >>= 1) {
+    __syncthreads();
+    if (w >= width && w < 2 * width) {
+      uint32_t *d = sh[w - width] + lane;
+      const uint32_t v[12] = {lo.x.c0, lo.x.c1, lo.y.c0, lo.y.c1, lo.z.c0, lo.z.c1,
+                              hi.x.c0, hi.x.c1, hi.y.c0, hi.y.c1, hi.z.c0, hi.z.c1};
+#pragma unroll
+      for (int k = 0; k < 12; k++) d[64 * k] = v[k];
+    }
+    __syncthreads();
+    if (w < width) {
+      const uint32_t *d = sh[w] + lane;
+      w4::J o;
+      o.x = {d[0], d[64]};
+      o.y = {d[128], d[192]};
+      o.z = {d[256], d[320]};
+      w4::add(c, lo, lo, o);
+      o.x = {d[384], d[448]};
+      o.y = {d[512], d[576]};
+      o.z = {d[640], d[704]};
+      w4::add(c, hi, hi, o);
+    }
+  }
+  if (w != 0) return;  // wave-uniform; no barrier follows
+#pragma unroll
+  for (int k = 1; k < NW; k++) err |= sh_err[k];
   if (empty_is_error && seg_off[s + 1] == seg_off[s]) err = 1;
   for (int d = 0; d < 32; d++) w4::dbl(c, hi, hi);
   w4::add(c, lo, lo, hi);
@@ -145,8 +183,9 @@ void launch_mv_g2mul_w4(hipStream_t st, const g2a *sigs, const uint64_t *rands, 
 void launch_g2sum_final_w4(hipStream_t st, const g2j *part, const int32_t *part_err, const uint32_t *chunks,
                            const uint32_t *seg_chunk, const uint32_t *seg_off, uint32_t nseg, uint32_t n,
                            int empty_is_error, g1s *P, g2a *H, int32_t *seg_err, g2j *Sj) {
-  (nseg <= w4::kExclusiveMaxWaves ? k_g2sum_final_w4<true> : k_g2sum_final_w4<false>)<<<nseg, 64, 0, st>>>(
-      part, part_err, chunks, seg_chunk, seg_off, nseg, n, empty_is_error, P, H, seg_err, Sj);
+  (nseg * kFinalW4Waves <= w4::kExclusiveMaxWaves ? k_g2sum_final_w4<true> : k_g2sum_final_w4<false>)<<<
+      nseg, 64 * kFinalW4Waves, 0, st>>>(part, part_err, chunks, seg_chunk, seg_off, nseg, n, empty_is_error, P, H,
+                                         seg_err, Sj);
 }
 
 }  // namespace gbls
