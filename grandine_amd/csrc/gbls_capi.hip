@@ -501,6 +501,7 @@ struct Engine {
   // Config::hold): the block shares the GPU only with the submissions already running
   bool block_hold = true;
   bool ml_pcn = true;         // the Miller kernel reads normalized points by column (GBLS_ML_PCN)
+  uint32_t g2sum_ch = WGR;    // sets per level-1 chunk of the signature sum (GBLS_G2SUM_CH)
   bool lines_s_main = false;  // experiments: the MSM pairs' lines on the main stream after the join,
   bool lines_s_lane = false;  // ... in the one-lane form
   std::atomic<int> block_active{0};
@@ -575,6 +576,7 @@ bool engine_init(uint32_t device_mask, uint32_t flags) {
       g.ml_rounds = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_SIDE2_HIGH")) g.side2_high = std::atoi(e) != 0;
     if (const char *e = std::getenv("GBLS_PRIO_MODE")) g.prio_mode = std::atoi(e);
+    if (const char *e = std::getenv("GBLS_G2SUM_CH")) g.g2sum_ch = std::max(16u, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char *e = std::getenv("GBLS_ROW_CLEAR_MAX"))
       g_row_clear_max = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GBLS_CU_SPLIT")) g.cu_split = std::atoi(e);
@@ -877,7 +879,7 @@ bool pipeline_partials(Ctx &c, Device &d, const uint8_t *msgs, const uint32_t *m
         });
   const size_t line_words = (size_t)mt.ncol * EC * 72;
   const size_t chunk_off = tab.size();
-  const uint32_t CH = WGR;  // sets per level-1 G2-sum workgroup
+  const uint32_t CH = g.g2sum_ch;  // sets per level-1 G2-sum workgroup (WGR unless GBLS_G2SUM_CH)
   std::vector<uint32_t> seg_chunk(nseg + 1, 0);
   for (size_t s = 0; s < nseg; s++) {
     seg_chunk[s] = (uint32_t)((tab.size() - chunk_off) / 4);
