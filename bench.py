@@ -96,11 +96,11 @@ def cpu_threads():
 def pmc_traffic(kernel, default_cmd):
     """HBM bytes per launch of `kernel` (a stage name: k_ml_group is the radix-2^28
     k_ml_group28 of the default build) from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
-    summary of the default command's 16-batch launches (profiles/r06/f_c2_pmc_bytes.csv,
+    summary of the default command's 16-batch launches (profiles/r06/g_c2_pmc_bytes.csv,
     tools/prof/pmc_bytes.py --largest; FETCH_SIZE doubled per the gfx950 correction).  None for
     other commands or if absent."""
     # the round's final pass, else its latest checkpoint pass
-    for tag in ("f", "z", "x", "o"):
+    for tag in ("g", "f", "z", "x", "o"):
         path = os.path.join(ROOT, "profiles", "r06", tag + "_c2_pmc_bytes.csv")
         if os.path.exists(path):
             break

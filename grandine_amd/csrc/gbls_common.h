@@ -126,10 +126,12 @@ struct MsmPlan {
   size_t o_cnt, o_start, o_cur, o_cstart, o_fstart[kMsmFoldLevels], o_list, o_chunk, o_t0, o_a0, o_t1, o_a1,
       o_sig28, bytes;
 };
-// default: segments at least this large use the bucket MSM (2048 -> 4096 in r04: a C4 epoch of
-// 2048-set segments ran 542-572k sets/s with per-set products vs 375-390k with the MSM,
-// profiles/r04/k_*; C2 and C5 segments are >= 4096)
-constexpr uint32_t kMsmMinPerSeg = 4096;
+// default: segments at least this large use the bucket MSM.  2048 -> 4096 in r04 (a C4 epoch of
+// 2048-set segments ran 542-572k sets/s with per-set products vs 375-390k with that round's MSM,
+// profiles/r04/k_*); back to 2048 in r06, after the radix-2^28 MSM and the lazy additions: C4
+// 546-575k with the MSM vs 511-557k with per-set products in two boxes, seven runs each way
+// (profiles/r06/zz_ab_msm_min.txt), C2 / C1 unchanged (their segments are >= 4096 / < 2048)
+constexpr uint32_t kMsmMinPerSeg = 2048;
 MsmPlan msm_plan(uint32_t n, uint32_t nseg);
 // writes each segment's p.extra Miller pairs (P[n + s * extra + k] = a constant G1 weight,
 // H[...] = affine bucket or window sum), zeroes seg_err and flags empty segments when
