@@ -48,7 +48,7 @@ static_assert(sizeof(fp12) == sizeof(gbls_fp12), "fp12 layout");
 
 uint32_t gbls::g_row_clear_max = gbls::kRowClearMax;
 uint32_t gbls::g_ml_r28 = 1;
-uint32_t gbls::g_msm_k = gbls::kMsmChunk;
+uint32_t gbls::g_msm_k = 0;  // chosen per plan (msm_plan) unless GBLS_MSM_K is set
 uint32_t gbls::g_msm_r28 = 1;
 uint32_t gbls::g_ml_xcd = 1;
 uint32_t gbls::g_ml_dma = 0;

@@ -42,9 +42,13 @@ extern uint32_t g_ml_r28;                // k_ml_group in radix-2^28 arithmetic 
 // (2271) -- within noise; the side-stream MSM overlaps the main chain, so its fill is not the
 // step's bound.  GBLS_MSM_K selects another K.
 constexpr uint32_t kMsmChunk = 16;
+// segments below 4096 sets (C4's 2048-set segments): K = 4, more and shorter chunk chains on the
+// signature side, which sets their join (C4 565-580k vs 529-566k with K = 16, one box,
+// profiles/r06/zz_ab_c4_msm_k.txt)
+constexpr uint32_t kMsmChunkSmall = 4;
 constexpr int kMsmFoldLevels = 3;        // k_msm_fold: pairwise levels over each bucket's partials
 constexpr uint32_t kMsmFold = 1u << kMsmFoldLevels;  // chunk partials per fold group
-extern uint32_t g_msm_k;                 // kMsmChunk unless GBLS_MSM_K is set
+extern uint32_t g_msm_k;                 // GBLS_MSM_K, else 0: kMsmChunkSmall / kMsmChunk (msm_plan)
 extern uint32_t g_msm_r28;               // k_msm_chunk28 / k_msm_fold28 (GBLS_MSM_R28=0: the engine-form kernels)
 extern uint32_t g_ml_kara;               // k_ml_group28: Karatsuba Fp2 sparse products (GBLS_ML_KARA)
 extern uint32_t g_ml_prefetch;           // k_ml_group28: next pair's line loaded during the product (GBLS_ML_PREFETCH)

@@ -410,8 +410,9 @@ MsmPlan msm_plan(uint32_t n, uint32_t nseg) {
   p.tree = p.c == 13;
   p.extra = p.tree ? (uint32_t)p.W : ((uint32_t)p.W << (p.c - 1));
   p.nb = nseg * ((uint32_t)p.W << (p.c - 1));
-  // chunks of <= K points (GBLS_MSM_K), fold groups of kMsmFold chunk partials
-  p.K = g_msm_k;
+  // chunks of <= K points (GBLS_MSM_K; else kMsmChunkSmall below 4096 sets per segment,
+  // kMsmChunk from there), fold groups of kMsmFold chunk partials
+  p.K = g_msm_k ? g_msm_k : (avg < 4096 ? kMsmChunkSmall : kMsmChunk);
   p.max_chunks = (uint32_t)(((uint64_t)p.W * n + p.K - 1) / p.K) + p.nb;
   p.max_folds = p.max_chunks / 2 + p.nb;
   size_t o = 0;
